@@ -1,0 +1,319 @@
+// Base field Fp of BLS12-381 for gfx950 (CDNA4) VALU.
+//
+// Representation: 14 limbs x 28 bits, Montgomery form with R = 2^392.  The limb width is chosen for
+// gfx950's integer pipes (measured, profiles/r01_valu_rates.json): v_mad_u64_u32 (32x32+64 -> 64)
+// issues at half rate, and so do the carry-flag adds (v_add_co/v_addc_co) -- but a 28-bit limb product
+// is < 2^56, so every Montgomery column (up to 28 products) is summed by plain v_mad_u64_u32 with NO
+// carry flags at all.  One Montgomery multiplication = 392 v_mad_u64_u32 (14^2 a*b + 14^2 m*p),
+// one squaring = 301.
+//
+// Value invariant for every stored element: 0 <= value <= 2p, limbs normalized (< 2^28, top limb holds
+// the rest).  fp_mul/fp_sqr outputs are < p + 2^-6 p.  Operands of fp_mul may be un-normalized sums
+// (`fp_add_nr`) of up to 4 invariant values (limbs < 2^30); fp_sqr accepts one level (limbs < 2^29).
+//
+// Reference semantics replaced: blst's vec384/mul_mont_384 family inside @chainsafe/blst@0.2.4
+// (reference yarn.lock:445-451) -- restated from the field definition, not translated.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define BLS_HD __host__ __device__ __forceinline__
+#define BLS_HDNI __host__ __device__ __noinline__
+#else
+#define BLS_HD static inline
+#define BLS_HDNI static
+#endif
+#define BLS_CONST static constexpr
+
+#define BLS_NL 14
+#define BLS_LB 28
+#define BLS_MASK 0x0FFFFFFFu
+
+struct fp {
+  uint32_t l[BLS_NL];
+};
+struct fp2 {
+  fp c0, c1;
+};
+
+#include "bls_constants.hpp"
+
+// ------------------------------------------------------------------------------------------------
+// Montgomery multiplication: finely integrated product scanning (column-wise a*b and m*p).
+// ------------------------------------------------------------------------------------------------
+BLS_HD fp fp_mul(const fp& a, const fp& b) {
+  fp r;
+  uint32_t m[BLS_NL];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < BLS_NL; k++) {
+#pragma unroll
+    for (int i = 0; i <= k; i++) acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+    for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * FP_P.l[k - i];
+    uint32_t mk = ((uint32_t)acc * BLS_N0INV) & BLS_MASK;
+    m[k] = mk;
+    acc += (uint64_t)mk * FP_P.l[0];
+    acc >>= BLS_LB;
+  }
+#pragma unroll
+  for (int k = BLS_NL; k < 2 * BLS_NL - 1; k++) {
+#pragma unroll
+    for (int i = k - BLS_NL + 1; i < BLS_NL; i++) {
+      acc += (uint64_t)a.l[i] * b.l[k - i];
+      acc += (uint64_t)m[i] * FP_P.l[k - i];
+    }
+    r.l[k - BLS_NL] = (uint32_t)acc & BLS_MASK;
+    acc >>= BLS_LB;
+  }
+  r.l[BLS_NL - 1] = (uint32_t)acc;
+  return r;
+}
+
+BLS_HD fp fp_sqr(const fp& a) {
+  fp r;
+  uint32_t m[BLS_NL];
+  uint32_t a2[BLS_NL];
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) a2[i] = a.l[i] << 1;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < BLS_NL; k++) {
+#pragma unroll
+    for (int i = 0; 2 * i < k; i++) acc += (uint64_t)a2[i] * a.l[k - i];
+    if ((k & 1) == 0) acc += (uint64_t)a.l[k >> 1] * a.l[k >> 1];
+#pragma unroll
+    for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * FP_P.l[k - i];
+    uint32_t mk = ((uint32_t)acc * BLS_N0INV) & BLS_MASK;
+    m[k] = mk;
+    acc += (uint64_t)mk * FP_P.l[0];
+    acc >>= BLS_LB;
+  }
+#pragma unroll
+  for (int k = BLS_NL; k < 2 * BLS_NL - 1; k++) {
+#pragma unroll
+    for (int i = k - BLS_NL + 1; 2 * i < k; i++) acc += (uint64_t)a2[i] * a.l[k - i];
+    if ((k & 1) == 0) acc += (uint64_t)a.l[k >> 1] * a.l[k >> 1];
+#pragma unroll
+    for (int i = k - BLS_NL + 1; i < BLS_NL; i++) acc += (uint64_t)m[i] * FP_P.l[k - i];
+    r.l[k - BLS_NL] = (uint32_t)acc & BLS_MASK;
+    acc >>= BLS_LB;
+  }
+  r.l[BLS_NL - 1] = (uint32_t)acc;
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Additive operations (keep value <= 2p, limbs normalized)
+// ------------------------------------------------------------------------------------------------
+// s (value <= 4p, normalized) -> s or s - 2p
+BLS_HD fp fp_csub_2p(const fp& s) {
+  fp t;
+  int32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL - 1; i++) {
+    int32_t v = (int32_t)s.l[i] - (int32_t)FP_2P.l[i] + bw;
+    t.l[i] = (uint32_t)v & BLS_MASK;
+    bw = v >> BLS_LB;
+  }
+  int32_t top = (int32_t)s.l[BLS_NL - 1] - (int32_t)FP_2P.l[BLS_NL - 1] + bw;
+  t.l[BLS_NL - 1] = (uint32_t)top;
+  const bool neg = top < 0;
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = neg ? s.l[i] : t.l[i];
+  return r;
+}
+
+BLS_HD fp fp_add(const fp& a, const fp& b) {
+  fp s;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL - 1; i++) {
+    uint32_t v = a.l[i] + b.l[i] + c;
+    s.l[i] = v & BLS_MASK;
+    c = v >> BLS_LB;
+  }
+  s.l[BLS_NL - 1] = a.l[BLS_NL - 1] + b.l[BLS_NL - 1] + c;
+  return fp_csub_2p(s);
+}
+
+// Un-normalized, un-reduced sum: only as an operand of fp_mul / fp_sqr (see header comment).
+BLS_HD fp fp_add_nr(const fp& a, const fp& b) {
+  fp s;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) s.l[i] = a.l[i] + b.l[i];
+  return s;
+}
+
+BLS_HD fp fp_sub(const fp& a, const fp& b) {
+  // a + 2p - b  in [0, 4p]  -> conditional subtract 2p
+  fp s;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL - 1; i++) {
+    int32_t v = (int32_t)a.l[i] + (int32_t)FP_2P.l[i] - (int32_t)b.l[i] + c;
+    s.l[i] = (uint32_t)v & BLS_MASK;
+    c = v >> BLS_LB;
+  }
+  s.l[BLS_NL - 1] = (uint32_t)((int32_t)a.l[BLS_NL - 1] + (int32_t)FP_2P.l[BLS_NL - 1] - (int32_t)b.l[BLS_NL - 1] + c);
+  return fp_csub_2p(s);
+}
+
+BLS_HD fp fp_neg(const fp& a) {
+  // 2p - a in [0, 2p]
+  fp s;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL - 1; i++) {
+    int32_t v = (int32_t)FP_2P.l[i] - (int32_t)a.l[i] + c;
+    s.l[i] = (uint32_t)v & BLS_MASK;
+    c = v >> BLS_LB;
+  }
+  s.l[BLS_NL - 1] = (uint32_t)((int32_t)FP_2P.l[BLS_NL - 1] - (int32_t)a.l[BLS_NL - 1] + c);
+  return s;
+}
+
+BLS_HD fp fp_dbl(const fp& a) { return fp_add(a, a); }
+
+// a / 2 (mod p): make even by adding p when odd, then shift right one bit.
+BLS_HD fp fp_half(const fp& a) {
+  const uint32_t odd = 0u - (a.l[0] & 1u);
+  fp s;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL - 1; i++) {
+    uint32_t v = a.l[i] + (FP_P.l[i] & odd) + c;
+    s.l[i] = v & BLS_MASK;
+    c = v >> BLS_LB;
+  }
+  s.l[BLS_NL - 1] = a.l[BLS_NL - 1] + (FP_P.l[BLS_NL - 1] & odd) + c;  // value <= 3p
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL - 1; i++) r.l[i] = (s.l[i] >> 1) | ((s.l[i + 1] & 1u) << (BLS_LB - 1));
+  r.l[BLS_NL - 1] = s.l[BLS_NL - 1] >> 1;
+  return r;  // value <= 1.5p
+}
+
+// small multiples (value <= 2p in, <= 2p out)
+BLS_HD fp fp_mul3(const fp& a) { return fp_add(fp_dbl(a), a); }
+BLS_HD fp fp_mul4(const fp& a) { return fp_dbl(fp_dbl(a)); }
+BLS_HD fp fp_mul8(const fp& a) { return fp_dbl(fp_mul4(a)); }
+
+BLS_HD fp fp_zero() {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = 0;
+  return r;
+}
+BLS_HD fp fp_one() { return FP_ONE; }
+
+// Canonical representative in [0, p)
+BLS_HD fp fp_csub_p(const fp& s) {
+  fp t;
+  int32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL - 1; i++) {
+    int32_t v = (int32_t)s.l[i] - (int32_t)FP_P.l[i] + bw;
+    t.l[i] = (uint32_t)v & BLS_MASK;
+    bw = v >> BLS_LB;
+  }
+  int32_t top = (int32_t)s.l[BLS_NL - 1] - (int32_t)FP_P.l[BLS_NL - 1] + bw;
+  t.l[BLS_NL - 1] = (uint32_t)top;
+  const bool neg = top < 0;
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = neg ? s.l[i] : t.l[i];
+  return r;
+}
+BLS_HD fp fp_canon(const fp& a) { return fp_csub_p(fp_csub_p(a)); }
+
+BLS_HD bool fp_is_zero(const fp& a) {
+  fp c = fp_canon(a);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) o |= c.l[i];
+  return o == 0;
+}
+
+BLS_HD bool fp_eq(const fp& a, const fp& b) { return fp_is_zero(fp_sub(a, b)); }
+
+BLS_HD fp fp_select(bool c, const fp& a, const fp& b) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = c ? a.l[i] : b.l[i];
+  return r;
+}
+
+// Montgomery conversions
+BLS_HD fp fp_to_mont(const fp& plain) { return fp_mul(plain, FP_R2); }
+BLS_HD fp fp_from_mont(const fp& a) {
+  fp one = fp_zero();
+  one.l[0] = 1;
+  return fp_canon(fp_mul(a, one));
+}
+
+// Exponentiation by a public constant (left-to-right binary; wave-uniform branches).
+BLS_HDNI fp fp_pow_words(const fp& a, const uint32_t* e, int nbits) {
+  fp r = a;
+  for (int i = nbits - 2; i >= 0; i--) {
+    r = fp_sqr(r);
+    if ((e[i >> 5] >> (i & 31)) & 1u) r = fp_mul(r, a);
+  }
+  return r;
+}
+
+BLS_HD fp fp_inv(const fp& a) { return fp_pow_words(a, EXP_P_MINUS_2, 381); }   // 0 -> 0
+BLS_HD fp fp_pow_p34(const fp& a) { return fp_pow_words(a, EXP_P_MINUS_3_DIV_4, 379); }
+
+// Big-endian 48-byte <-> canonical integer limbs (not Montgomery).  Returns false if value >= p.
+BLS_HD bool fp_from_be48_plain(const uint8_t* b, fp& out, uint8_t top_mask) {
+  // bits: byte b[47 - j] holds bits 8j..8j+7
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) out.l[i] = 0;
+#pragma unroll
+  for (int j = 0; j < 48; j++) {
+    uint32_t byte = b[47 - j];
+    if (j == 47) byte &= top_mask;
+    int bit = 8 * j;
+    int li = bit / BLS_LB, off = bit % BLS_LB;
+    out.l[li] |= (byte << off) & BLS_MASK;
+    if (off > BLS_LB - 8 && li + 1 < BLS_NL) out.l[li + 1] |= byte >> (BLS_LB - off);
+  }
+  // compare with p
+  int32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    int32_t v = (int32_t)out.l[i] - (int32_t)FP_P.l[i] + bw;
+    bw = v >> BLS_LB;
+  }
+  return bw < 0;  // value < p
+}
+
+BLS_HD void fp_to_be48_plain(const fp& canon, uint8_t* b) {
+#pragma unroll
+  for (int j = 0; j < 48; j++) {
+    int bit = 8 * j;
+    int li = bit / BLS_LB, off = bit % BLS_LB;
+    uint32_t v = canon.l[li] >> off;
+    if (off > BLS_LB - 8 && li + 1 < BLS_NL) v |= canon.l[li + 1] << (BLS_LB - off);
+    b[47 - j] = (uint8_t)v;
+  }
+}
+
+// value > (p-1)/2 for a canonical plain value  (ZCash "lexicographically largest")
+BLS_HD bool fp_plain_gt_half(const fp& canon) {
+  // compute 2*v - p: v > (p-1)/2  <=>  2v > p - 1  <=>  2v >= p
+  int32_t bw = 0;
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    uint32_t d = (canon.l[i] << 1) + carry;
+    carry = d >> BLS_LB;
+    if (i < BLS_NL - 1) d &= BLS_MASK;
+    int32_t v = (int32_t)d - (int32_t)FP_P.l[i] + bw;
+    bw = v >> BLS_LB;
+  }
+  return bw >= 0;
+}

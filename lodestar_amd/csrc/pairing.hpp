@@ -1,0 +1,97 @@
+// Optimal-ate Miller loop and final exponentiation for BLS12-381.  Same algorithm as
+// oracle/bls12_381.py `miller_loop_proj` / `final_exp` (the oracle checks it against the definitional
+// affine Miller loop and the definitional (p^12-1)/r exponentiation).
+#pragma once
+#include "curve.hpp"
+
+struct g2proj {
+  fp2 x, y, z;
+};
+
+// Doubling step in homogeneous projective coordinates with the tangent line evaluated at P:
+//   line = (E - B) + (3 X^2 xP) v + (-H yP) v w
+BLS_HD void miller_dbl_step(g2proj& T, const fp& xP, const fp& yP, fp2& l0, fp2& l1, fp2& l4) {
+  fp2 A = fp2_half(fp2_mul(T.x, T.y));
+  fp2 B = fp2_sqr(T.y);
+  fp2 C = fp2_sqr(T.z);
+  // E = 3 b' C = 12 (1+u) C
+  fp2 E = fp2_mul3(fp2_mul_xi(C));
+  E = fp2_dbl(fp2_dbl(E));
+  fp2 F = fp2_mul3(E);
+  fp2 G = fp2_half(fp2_add(B, F));
+  fp2 H = fp2_sub(fp2_sub(fp2_sqr(fp2_add(T.y, T.z)), B), C);
+  fp2 J = fp2_sqr(T.x);
+  fp2 E2 = fp2_sqr(E);
+  T.x = fp2_mul(A, fp2_sub(B, F));
+  T.y = fp2_sub(fp2_sqr(G), fp2_mul3(E2));
+  T.z = fp2_mul(B, H);
+  l0 = fp2_sub(E, B);
+  l1 = fp2_mul_fp(fp2_mul3(J), xP);
+  l4 = fp2_mul_fp(fp2_neg(H), yP);
+}
+
+// Mixed addition step T + Q (Q affine) with the chord line evaluated at P:
+//   line = (theta x2 - lambda y2) + (-theta xP) v + (lambda yP) v w
+BLS_HD void miller_add_step(g2proj& T, const g2a& Q, const fp& xP, const fp& yP, fp2& l0, fp2& l1, fp2& l4) {
+  fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
+  fp2 lam = fp2_sub(T.x, fp2_mul(Q.x, T.z));
+  fp2 C = fp2_sqr(theta);
+  fp2 D = fp2_sqr(lam);
+  fp2 E = fp2_mul(lam, D);
+  fp2 F = fp2_mul(T.z, C);
+  fp2 G = fp2_mul(T.x, D);
+  fp2 H = fp2_sub(fp2_add(E, F), fp2_dbl(G));
+  fp2 X3 = fp2_mul(lam, H);
+  fp2 Y3 = fp2_sub(fp2_mul(theta, fp2_sub(G, H)), fp2_mul(T.y, E));
+  fp2 Z3 = fp2_mul(T.z, E);
+  l0 = fp2_sub(fp2_mul(theta, Q.x), fp2_mul(lam, Q.y));
+  l1 = fp2_mul_fp(fp2_neg(theta), xP);
+  l4 = fp2_mul_fp(lam, yP);
+  T.x = X3;
+  T.y = Y3;
+  T.z = Z3;
+}
+
+// f = conj(f_{|z|,Q}(P)).  P, Q affine and not infinity.
+BLS_HDNI fp12 miller_loop(const g1a& P, const g2a& Q) {
+  g2proj T;
+  T.x = Q.x;
+  T.y = Q.y;
+  T.z = fp2_one();
+  fp12 f = fp12_one();
+  fp2 l0, l1, l4;
+  // top bit (63) of |z| consumed by T = Q
+  for (int i = 62; i >= 0; i--) {
+    if (i != 62) f = fp12_sqr(f);
+    miller_dbl_step(T, P.x, P.y, l0, l1, l4);
+    f = fp12_mul_by_014(f, l0, l1, l4);
+    if ((BLS_Z_ABS >> i) & 1ull) {
+      miller_add_step(T, Q, P.x, P.y, l0, l1, l4);
+      f = fp12_mul_by_014(f, l0, l1, l4);
+    }
+  }
+  return fp12_conj(f);
+}
+
+// f^|z| (plain square-and-multiply; f in the cyclotomic subgroup after the easy part)
+BLS_HDNI fp12 fp12_pow_zabs(const fp12& f) {
+  fp12 r = f;
+  for (int i = 62; i >= 0; i--) {
+    r = fp12_sqr(r);
+    if ((BLS_Z_ABS >> i) & 1ull) r = fp12_mul(r, f);
+  }
+  return r;
+}
+BLS_HD fp12 fp12_pow_z(const fp12& f) { return fp12_conj(fp12_pow_zabs(f)); }
+
+// Final exponentiation, returns e^3 (same "== 1" answer since gcd(3, r) = 1):
+//   easy part (p^6 - 1)(p^2 + 1), hard part 3(p^4 - p^2 + 1)/r = (z-1)^2 (z+p)(z^2+p^2-1) + 3
+BLS_HDNI fp12 final_exponentiation(const fp12& f) {
+  fp12 f1 = fp12_mul(fp12_conj(f), fp12_inv(f));
+  fp12 m = fp12_mul(fp12_frob2(f1), f1);
+  fp12 t = fp12_mul(fp12_pow_z(m), fp12_conj(m));
+  t = fp12_mul(fp12_pow_z(t), fp12_conj(t));
+  t = fp12_mul(fp12_pow_z(t), fp12_frob1(t));
+  t = fp12_mul(fp12_mul(fp12_pow_z(fp12_pow_z(t)), fp12_frob2(t)), fp12_conj(t));
+  return fp12_mul(t, fp12_mul(fp12_sqr(m), m));
+}

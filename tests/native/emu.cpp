@@ -1,0 +1,124 @@
+// TEST HARNESS ONLY: compiles the per-element device logic (lodestar_amd/csrc/*.hpp) for the host CPU
+// so tests can check the exact kernel arithmetic against the oracle without a GPU.  It is never linked
+// into libblsgpu.so (the product has no CPU path).  Byte formats: canonical big-endian 48-byte Fp.
+#include <string.h>
+#include "../../lodestar_amd/csrc/ops.hpp"
+
+static fp load_mont(const uint8_t* b) {
+  fp x;
+  fp_from_be48_plain(b, x, 0xff);
+  return fp_to_mont(x);
+}
+static fp2 load2(const uint8_t* b) { return fp2_make(load_mont(b + 48), load_mont(b)); }  // c1||c0
+static void store2(const fp2& a, uint8_t* b) {
+  fp_to_be48(a.c1, b);
+  fp_to_be48(a.c0, b + 48);
+}
+static g2a load_g2(const uint8_t* b) {
+  g2a p;
+  p.x = load2(b);
+  p.y = load2(b + 96);
+  return p;
+}
+static g1a load_g1(const uint8_t* b) {
+  g1a p;
+  p.x = load_mont(b);
+  p.y = load_mont(b + 48);
+  return p;
+}
+// Fp12 -> 12 x 48 bytes, tower order c0.c0.c0, c0.c0.c1, c0.c1.c0, ... c1.c2.c1
+static void store12(const fp12& f, uint8_t* b) {
+  const fp6* s[2] = {&f.c0, &f.c1};
+  int k = 0;
+  for (int i = 0; i < 2; i++) {
+    const fp2* t[3] = {&s[i]->c0, &s[i]->c1, &s[i]->c2};
+    for (int j = 0; j < 3; j++) {
+      fp_to_be48(t[j]->c0, b + 48 * k++);
+      fp_to_be48(t[j]->c1, b + 48 * k++);
+    }
+  }
+}
+static fp12 load12(const uint8_t* b) {
+  fp12 f;
+  fp6* s[2] = {&f.c0, &f.c1};
+  int k = 0;
+  for (int i = 0; i < 2; i++) {
+    fp2* t[3] = {&s[i]->c0, &s[i]->c1, &s[i]->c2};
+    for (int j = 0; j < 3; j++) {
+      t[j]->c0 = load_mont(b + 48 * k++);
+      t[j]->c1 = load_mont(b + 48 * k++);
+    }
+  }
+  return f;
+}
+
+extern "C" {
+void emu_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp_to_be48(fp_mul(load_mont(a), load_mont(b)), out); }
+void emu_fp_sqr(const uint8_t* a, uint8_t* out) { fp_to_be48(fp_sqr(load_mont(a)), out); }
+void emu_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp_to_be48(fp_add(load_mont(a), load_mont(b)), out); }
+void emu_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp_to_be48(fp_sub(load_mont(a), load_mont(b)), out); }
+void emu_fp_inv(const uint8_t* a, uint8_t* out) { fp_to_be48(fp_inv(load_mont(a)), out); }
+void emu_fp_half(const uint8_t* a, uint8_t* out) { fp_to_be48(fp_half(load_mont(a)), out); }
+int emu_fp2_sqrt(const uint8_t* a, uint8_t* out) {
+  fp2 r;
+  bool ok = fp2_sqrt(load2(a), r);
+  store2(r, out);
+  return ok;
+}
+void emu_fp2_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { store2(fp2_mul(load2(a), load2(b)), out); }
+void emu_fp2_sqr(const uint8_t* a, uint8_t* out) { store2(fp2_sqr(load2(a)), out); }
+void emu_fp2_inv(const uint8_t* a, uint8_t* out) { store2(fp2_inv(load2(a)), out); }
+int emu_sig_decode(const uint8_t* b, uint32_t len, uint8_t* out192, int* inf) {
+  g2a p;
+  bool is_inf;
+  int st = sig_decode(b, len, p, is_inf);
+  *inf = is_inf;
+  if (st == 0 && !is_inf) g2a_to_be192(p, out192);
+  return st;
+}
+int emu_pk_decode(const uint8_t* b, uint8_t* out96) {
+  g1a p;
+  bool inf;
+  int st = pk_decode96(b, p, inf);
+  if (st == 0 && !inf) g1a_to_be96(p, out96);
+  return st;
+}
+void emu_expand_message(const uint8_t* msg, uint8_t* out256) {
+  uint32_t w[64];
+  expand_message_xmd_32(msg, w);
+  for (int i = 0; i < 64; i++)
+    for (int j = 0; j < 4; j++) out256[4 * i + j] = (uint8_t)(w[i] >> (24 - 8 * j));
+}
+void emu_hash_to_field(const uint8_t* msg, uint8_t* out192) {
+  fp2 u0, u1;
+  hash_to_field_fp2x2(msg, u0, u1);
+  store2(u0, out192);
+  store2(u1, out192 + 96);
+}
+int emu_hash_to_g2(const uint8_t* msg, uint8_t* out192) {
+  g2j h = hash_to_g2_jac(msg);
+  g2a a;
+  if (!jac_to_aff(h, a)) return 0;
+  g2a_to_be192(a, out192);
+  return 1;
+}
+int emu_g2_in_subgroup(const uint8_t* p192) { return g2_in_subgroup(load_g2(p192)); }
+int emu_g2_mul_u64(const uint8_t* p192, uint64_t k, uint8_t* out192) {
+  g2a a;
+  if (!jac_to_aff(jac_mul_u64(load_g2(p192), k), a)) return 0;
+  g2a_to_be192(a, out192);
+  return 1;
+}
+int emu_g1_mul_u64(const uint8_t* p96, uint64_t k, uint8_t* out96) {
+  g1a a;
+  if (!jac_to_aff(jac_mul_u64(load_g1(p96), k), a)) return 0;
+  g1a_to_be96(a, out96);
+  return 1;
+}
+void emu_miller(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) { store12(miller_loop(load_g1(p96), load_g2(q192)), out576); }
+void emu_final_exp(const uint8_t* f576, uint8_t* out576) { store12(final_exponentiation(load12(f576)), out576); }
+void emu_fp12_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { store12(fp12_mul(load12(a), load12(b)), out); }
+void emu_fp12_sqr(const uint8_t* a, uint8_t* out) { store12(fp12_sqr(load12(a)), out); }
+void emu_fp12_inv(const uint8_t* a, uint8_t* out) { store12(fp12_inv(load12(a)), out); }
+void emu_fp12_frob1(const uint8_t* a, uint8_t* out) { store12(fp12_frob1(load12(a)), out); }
+}

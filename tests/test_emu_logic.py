@@ -1,0 +1,167 @@
+"""The device arithmetic (lodestar_amd/csrc/*.hpp), compiled for the host CPU by tests/native/emu.cpp,
+checked against the oracle.  Same source as the HIP kernels; the GPU parity tests re-check it on MI355X."""
+import ctypes
+import random
+
+import pytest
+
+from oracle import bls12_381 as bls
+from tests.emu_helpers import (b2f12, b2f2, b2g1, b2g2, f12b, f2b, fpb, fromb, g1b, g2b, lib)
+
+P = bls.P
+rnd = random.Random(1234)
+
+
+def buf(n):
+    return ctypes.create_string_buffer(n)
+
+
+def edge_fp():
+    return [0, 1, 2, P - 1, P - 2, (P - 1) // 2, (P + 1) // 2, 2**380, 2**381 - 1 - P if 2**381 > P else 5,
+            0xFFFFFFF, 1 << 28, (1 << 364) - 1] + [rnd.randrange(P) for _ in range(40)]
+
+
+def test_fp_ops():
+    L = lib()
+    vals = edge_fp()
+    o = buf(48)
+    for a in vals:
+        for b in vals[:12] + [rnd.randrange(P) for _ in range(3)]:
+            L.emu_fp_mul(fpb(a), fpb(b), o)
+            assert fromb(o.raw) == a * b % P, (a, b)
+            L.emu_fp_add(fpb(a), fpb(b), o)
+            assert fromb(o.raw) == (a + b) % P
+            L.emu_fp_sub(fpb(a), fpb(b), o)
+            assert fromb(o.raw) == (a - b) % P
+        L.emu_fp_sqr(fpb(a), o)
+        assert fromb(o.raw) == a * a % P
+        L.emu_fp_half(fpb(a), o)
+        assert fromb(o.raw) * 2 % P == a % P
+    for a in vals[:10]:
+        L.emu_fp_inv(fpb(a), o)
+        assert fromb(o.raw) == (pow(a, P - 2, P))
+
+
+def test_fp2_ops_and_sqrt():
+    L = lib()
+    o = buf(96)
+    cases = [(0, 0), (1, 0), (0, 1), (P - 1, 0), (0, P - 1), (4, 0), (5, 0)] + [
+        (rnd.randrange(P), rnd.randrange(P)) for _ in range(30)
+    ] + [(rnd.randrange(P), 0) for _ in range(6)] + [(0, rnd.randrange(P)) for _ in range(6)]
+    for a in cases:
+        b = (rnd.randrange(P), rnd.randrange(P))
+        L.emu_fp2_mul(f2b(a), f2b(b), o)
+        assert b2f2(o.raw) == bls.f2mul(a, b)
+        L.emu_fp2_sqr(f2b(a), o)
+        assert b2f2(o.raw) == bls.f2sqr(a)
+        if a != (0, 0):
+            L.emu_fp2_inv(f2b(a), o)
+            assert bls.f2mul(b2f2(o.raw), a) == (1, 0)
+        ok = L.emu_fp2_sqrt(f2b(a), o)
+        assert bool(ok) == bls.f2_is_square(a), a
+        if ok:
+            assert bls.f2sqr(b2f2(o.raw)) == a
+
+
+def test_fp12_ops():
+    L = lib()
+    rf2 = lambda: (rnd.randrange(P), rnd.randrange(P))
+    rf12 = lambda: ((rf2(), rf2(), rf2()), (rf2(), rf2(), rf2()))
+    o = buf(576)
+    for _ in range(3):
+        a, b = rf12(), rf12()
+        L.emu_fp12_mul(f12b(a), f12b(b), o)
+        assert b2f12(o.raw) == bls.f12mul(a, b)
+        L.emu_fp12_sqr(f12b(a), o)
+        assert b2f12(o.raw) == bls.f12sqr(a)
+        L.emu_fp12_inv(f12b(a), o)
+        assert b2f12(o.raw) == bls.f12inv(a)
+        L.emu_fp12_frob1(f12b(a), o)
+        assert b2f12(o.raw) == bls.f12frob(a, 1)
+
+
+def test_expand_and_hash_to_field():
+    import os
+    L = lib()
+    o = buf(256)
+    for i in range(5):
+        msg = os.urandom(32) if i else bytes(32)
+        L.emu_expand_message(msg, o)
+        assert o.raw == bls.expand_message_xmd(msg, bls.DST_POP, 256)
+        o2 = buf(192)
+        L.emu_hash_to_field(msg, o2)
+        u0, u1 = bls.hash_to_field_fp2(msg, 2)
+        assert b2f2(o2.raw[:96]) == u0 and b2f2(o2.raw[96:]) == u1
+
+
+def test_hash_to_g2():
+    L = lib()
+    o = buf(192)
+    for i in range(4):
+        msg = bytes([i]) * 32
+        assert L.emu_hash_to_g2(msg, o) == 1
+        assert b2g2(o.raw) == bls.hash_to_g2(msg)
+
+
+def test_subgroup_and_scalar_mul():
+    L = lib()
+    o = buf(192)
+    Q = bls.g2_mul(bls.G2_GEN, 987654321)
+    assert L.emu_g2_in_subgroup(g2b(Q)) == 1
+    # random non-subgroup point
+    while True:
+        x = (rnd.randrange(P), rnd.randrange(P))
+        y = bls.f2sqrt(bls.f2add(bls.f2mul(bls.f2sqr(x), x), bls.B2))
+        if y:
+            break
+    assert L.emu_g2_in_subgroup(g2b((x, y))) == 0
+    for k in [1, 2, 3, 0xFFFFFFFFFFFFFFFF, rnd.getrandbits(64)]:
+        assert L.emu_g2_mul_u64(g2b(Q), k, o) == 1
+        assert b2g2(o.raw) == bls.g2_mul(Q, k)
+        o1 = buf(96)
+        Pp = bls.g1_mul(bls.G1_GEN, 5555)
+        assert L.emu_g1_mul_u64(g1b(Pp), k, o1) == 1
+        assert b2g1(o1.raw) == bls.g1_mul(Pp, k)
+
+
+def test_miller_and_final_exp():
+    L = lib()
+    Pp = bls.g1_mul(bls.G1_GEN, 12345)
+    Q = bls.g2_mul(bls.G2_GEN, 678)
+    o = buf(576)
+    L.emu_miller(g1b(Pp), g2b(Q), o)
+    f = b2f12(o.raw)
+    assert f == bls.miller_loop(Pp, Q)
+    o2 = buf(576)
+    L.emu_final_exp(f12b(f), o2)
+    assert b2f12(o2.raw) == bls.final_exp(f)
+
+
+def test_sig_decode_classes():
+    L = lib()
+    o = buf(192)
+    inf = ctypes.c_int()
+    sk = 0x1234567
+    sig = bls.sign(sk, b"\x07" * 32)
+    comp = bls.g2_compress(sig)
+    unc = bls.g2_serialize(sig)
+    assert L.emu_sig_decode(comp, 96, o, ctypes.byref(inf)) == 0 and b2g2(o.raw) == sig
+    assert L.emu_sig_decode(unc, 192, o, ctypes.byref(inf)) == 0 and b2g2(o.raw) == sig
+    cases = {
+        bytes(32): bls.BLST_INVALID_SIZE,
+        bytes([0xC0]) + bytes(95): 0,
+        bytes([0xE0]) + bytes(95): bls.BLST_BAD_ENCODING,
+        bytes([0xC0]) + bytes(94) + b"\x01": bls.BLST_BAD_ENCODING,
+        comp[:1].replace(comp[:1], bytes([comp[0] & 0x7F])) + comp[1:]: bls.BLST_BAD_ENCODING,
+        bytes([0x9A]) + b"\xff" * 95: bls.BLST_BAD_ENCODING,  # x1 >= p
+    }
+    # non-residue x
+    for t in range(1, 50):
+        xb = bytes([0x80]) + bytes(46) + bytes([t]) + bytes(48)
+        code = bls.classify_signature(xb)
+        cases[xb] = code
+    for b, want in cases.items():
+        got = L.emu_sig_decode(b, len(b), o, ctypes.byref(inf))
+        assert got == bls.classify_signature(b) == want, (b.hex(), got, want)
+    codes = set(cases.values())
+    assert bls.BLST_POINT_NOT_ON_CURVE in codes and bls.BLST_POINT_NOT_IN_GROUP in codes
