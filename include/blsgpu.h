@@ -1,0 +1,120 @@
+/* blsgpu.h -- C ABI of the MI355X BLS12-381 signature-set verifier (libblsgpu.so).
+ *
+ * Drop-in boundary for Lodestar's IBlsVerifier path.  The entry points replace, one for one, what the
+ * reference reaches through @chainsafe/bls / @chainsafe/blst from its worker pool:
+ *
+ *   blsgpu_verify / blsgpu_submit  <- BlsMultiThreadWorkerPool.verifySignatureSets
+ *                                      (reference packages/beacon-node/src/chain/bls/multithread/index.ts:134-174)
+ *                                      + worker verifyManySignatureSets (multithread/worker.ts:32-108)
+ *                                      + verifySignatureSetsMaybeBatch (chain/bls/maybeBatch.ts:16-39)
+ *   pk_bytes / set_pk_first+pk_index <- getAggregatedPubkey(set).toBytes(uncompressed) (multithread/index.ts:160,
+ *                                      chain/bls/utils.ts:5-16); table mode aggregates on the GPU instead
+ *   blsgpu_pubkeys_upload           <- the pubkey cache the sets draw from (state-transition
+ *                                      src/cache/pubkeyCache.ts:56-77, epochContext.ts:702-705)
+ *   blsgpu_destroy                  <- IBlsVerifier.close (chain/bls/interface.ts:45)
+ *
+ * Conventions: plain pointers and sizes, caller-owned buffers, every call copies its inputs before
+ * returning (blsgpu_submit included), `int` status (0 = ok).  Per-job results use the blst error names
+ * thrown by @chainsafe/blst: result 1 = valid, 0 = invalid (a well-formed signature that does not
+ * verify), negative = -(BLSGPU_* error code) -> the JS side rejects the job's promise with
+ * Error("BLST_ERROR: <name>") exactly where the reference throws.
+ */
+#ifndef BLSGPU_H
+#define BLSGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BLSGPU_ABI_VERSION 1
+
+enum blsgpu_code {
+  BLSGPU_OK = 0,
+  BLSGPU_BAD_ENCODING = 1,       /* BLST_BAD_ENCODING */
+  BLSGPU_POINT_NOT_ON_CURVE = 2, /* BLST_POINT_NOT_ON_CURVE */
+  BLSGPU_POINT_NOT_IN_GROUP = 3, /* BLST_POINT_NOT_IN_GROUP */
+  BLSGPU_AGGR_TYPE_MISMATCH = 4, /* BLST_AGGR_TYPE_MISMATCH (unused on this path) */
+  BLSGPU_VERIFY_FAIL = 5,        /* BLST_VERIFY_FAIL (unused on this path) */
+  BLSGPU_PK_IS_INFINITY = 6,     /* BLST_PK_IS_INFINITY */
+  BLSGPU_BAD_SCALAR = 7,         /* BLST_BAD_SCALAR (unused on this path) */
+  BLSGPU_INVALID_SIZE = 8,       /* BLST_INVALID_SIZE: signature not 96/192 bytes (multithread.test.ts:100) */
+  BLSGPU_EMPTY_AGGREGATE = 9,    /* EMPTY_AGGREGATE_ARRAY: aggregate set with pubkeys = [] */
+  BLSGPU_EMPTY_SET = 10,         /* "Empty signature set" (maybeBatch.ts:29-31) */
+  BLSGPU_DEVICE_ERROR = 11,      /* HIP failure: every job of the call is rejected, never `false` */
+  BLSGPU_ERR_ARGS = 100,         /* call-level: malformed arguments */
+  BLSGPU_ERR_NO_DEVICE = 101,    /* call-level: no usable MI355X */
+  BLSGPU_ERR_CLOSED = 102        /* call-level: context destroyed (QUEUE_ERROR_QUEUE_ABORTED) */
+};
+
+typedef struct blsgpu_ctx blsgpu_ctx;
+
+/* One verifySignatureSets submission: n_jobs jobs over n_sets signature sets.  Job j owns sets
+ * [job_first_set[j], job_first_set[j+1]).  A job resolves true iff every one of its sets verifies;
+ * jobs never affect each other's outcome (the reference's per-job isolation, worker.ts:76-98). */
+typedef struct blsgpu_batch {
+  uint32_t n_sets;
+  uint32_t n_jobs;
+  const uint32_t* job_first_set; /* [n_jobs + 1], non-decreasing, job_first_set[n_jobs] == n_sets */
+  const uint8_t* job_flags;      /* [n_jobs] bit0 = batchable (VerifySignatureOpts.batchable); NULL = none */
+  /* Public keys, one of two modes:
+   *  bytes mode: pk_bytes[96 * i] = set i's (already aggregated) pubkey, uncompressed affine (ZCash);
+   *  table mode: set i aggregates table entries pk_index[set_pk_first[i] .. set_pk_first[i+1]). */
+  const uint8_t* pk_bytes;
+  const uint32_t* set_pk_first; /* [n_sets + 1] */
+  const uint32_t* pk_index;
+  const uint8_t* msgs;     /* [32 * n_sets] signing roots */
+  const uint8_t* sigs;     /* [sig_stride * n_sets] untrusted signature bytes */
+  const uint32_t* sig_len; /* [n_sets]: 96 (compressed) or 192 (uncompressed); else BLST_INVALID_SIZE */
+  uint32_t sig_stride;
+  uint64_t seed; /* random-linear-combination scalars: fixed seed for comparison runs, 0 = OS CSPRNG */
+} blsgpu_batch;
+
+typedef struct blsgpu_stats {
+  uint32_t groups;             /* batch groups checked (one final exponentiation each) */
+  uint32_t batch_retries;      /* failed groups re-checked per job (metric blsThreadPool.batchRetries) */
+  uint32_t batch_sigs_success; /* sets accepted by a batch group (metric blsThreadPool.batchSigsSuccess) */
+  uint32_t devices_used;
+  double device_ms; /* wall time of the device phase (max over devices) */
+} blsgpu_stats;
+
+/* Create a context on the given HIP devices (NULL / n <= 0: every visible device). */
+int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out);
+/* Waits for in-flight submissions, fails queued ones with BLSGPU_ERR_CLOSED, frees everything. */
+void blsgpu_destroy(blsgpu_ctx* ctx);
+int blsgpu_device_count(const blsgpu_ctx* ctx);
+
+/* Trusted pubkey table (replicated on every device): entries [first_index, first_index + n) from
+ * 96-byte uncompressed affine encodings.  Returns BLSGPU_BAD_ENCODING / _POINT_NOT_ON_CURVE for a
+ * malformed entry (nothing is written in that case). */
+int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* pk96, uint32_t n);
+uint32_t blsgpu_pubkeys_count(const blsgpu_ctx* ctx);
+
+/* Synchronous verification.  job_result[n_jobs]: 1 valid / 0 invalid / -code.  Returns a call-level
+ * status (BLSGPU_OK even when some jobs are invalid or rejected). */
+int blsgpu_verify(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result, blsgpu_stats* stats);
+
+/* Asynchronous verification: inputs are copied before return; `done(user, status)` runs on a runtime
+ * thread once job_result / stats are written.  For the N-API addon's threadsafe-function bridge. */
+typedef void (*blsgpu_done_cb)(void* user, int status);
+int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result, blsgpu_stats* stats,
+                  blsgpu_done_cb done, void* user);
+
+/* Tunables: "group_sets" (target sets per batch group, default 64), "max_devices". */
+int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value);
+
+/* "BLST_INVALID_SIZE", ... for job codes; NULL for unknown codes. */
+const char* blsgpu_code_name(int code);
+
+/* Test hook: run one pipeline stage element-wise on device 0 (canonical big-endian encodings).
+ * op: 0 fp_mul(48,48->48) 1 sig_decode(192+len -> status,192) 2 hash_to_g2(32->192)
+ *     3 miller(96,192->576) 4 final_exp(576->576) 5 g1_mul_u64(96,8->96) 6 g2_mul_u64(192,8->192)
+ * Returns BLSGPU_OK or an error. */
+int blsgpu_debug_op(blsgpu_ctx* ctx, int op, uint32_t n, const uint8_t* in, uint32_t in_stride,
+                    uint8_t* out, uint32_t out_stride, int32_t* status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLSGPU_H */

@@ -1,0 +1,60 @@
+"""Builds lodestar_amd/libblsgpu.so (HIP kernels + C-ABI runtime) for gfx950 with hipcc, in-tree.
+
+    python -m lodestar_amd.build            # incremental
+    python -m lodestar_amd.build --force
+"""
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libblsgpu.so")
+ARCH = os.environ.get("BLSGPU_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+SOURCES = ["kernels.hip", "runtime.cpp"]
+
+
+def _deps():
+    out = [os.path.join(ROOT, "include", "blsgpu.h")]
+    for f in os.listdir(CSRC):
+        if f.endswith((".hpp", ".h", ".hip", ".cpp")):
+            out.append(os.path.join(CSRC, f))
+    return out
+
+
+def up_to_date():
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(d) <= t for d in _deps())
+
+
+def build(force=False, verbose=True):
+    if not force and up_to_date():
+        return LIB
+    objs = []
+    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include")]
+    procs = []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
+        objs.append(obj)
+        cmd = [HIPCC] + common + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd))
+    for p in procs:
+        if p.wait() != 0:
+            raise RuntimeError("hipcc failed")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", LIB] + objs + ["-lpthread"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

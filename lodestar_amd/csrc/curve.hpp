@@ -64,7 +64,7 @@ BLS_HD jac<F> jac_from_aff(const aff<F>& a) {
 }
 
 template <class F>
-BLS_HD jac<F> jac_dbl(const jac<F>& p) {
+BLS_FN jac<F> jac_dbl(const jac<F>& p) {
   F A = F_sqr(p.x);
   F B = F_sqr(p.y);
   F C = F_sqr(B);
@@ -183,7 +183,7 @@ BLS_HDNI bool jac_to_aff(const g2j& p, g2a& out) {
 
 // Jacobian equality (both may be infinity)
 template <class F>
-BLS_HD bool jac_eq(const jac<F>& p, const jac<F>& q) {
+BLS_FN bool jac_eq(const jac<F>& p, const jac<F>& q) {
   bool pi = jac_is_inf(p), qi = jac_is_inf(q);
   if (pi || qi) return pi && qi;
   F Z1Z1 = F_sqr(p.z), Z2Z2 = F_sqr(q.z);
@@ -194,14 +194,14 @@ BLS_HD bool jac_eq(const jac<F>& p, const jac<F>& q) {
 }
 
 // ---- G2 endomorphism psi and subgroup check -------------------------------------------------------
-BLS_HD g2j g2_psi(const g2j& p) {
+BLS_FN g2j g2_psi(const g2j& p) {
   g2j r;
   r.x = fp2_mul(fp2_conj(p.x), PSI_X);
   r.y = fp2_mul(fp2_conj(p.y), PSI_Y);
   r.z = fp2_conj(p.z);
   return r;
 }
-BLS_HD g2j g2_psi2(const g2j& p) {
+BLS_FN g2j g2_psi2(const g2j& p) {
   g2j r;
   r.x = fp2_mul(p.x, PSI2_X);
   r.y = fp2_mul(p.y, PSI2_Y);

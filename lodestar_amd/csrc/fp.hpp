@@ -20,9 +20,13 @@
 #include <hip/hip_runtime.h>
 #define BLS_HD __host__ __device__ __forceinline__
 #define BLS_HDNI __host__ __device__ __noinline__
+// Medium/large arithmetic (a Montgomery product is ~450 instructions) is emitted once as a real device
+// function: inlining everything into every kernel makes multi-hour compiles of multi-MB code objects.
+#define BLS_FN __host__ __device__ __noinline__
 #else
 #define BLS_HD static inline
 #define BLS_HDNI static
+#define BLS_FN static
 #endif
 #define BLS_CONST static constexpr
 
@@ -42,7 +46,7 @@ struct fp2 {
 // ------------------------------------------------------------------------------------------------
 // Montgomery multiplication: finely integrated product scanning (column-wise a*b and m*p).
 // ------------------------------------------------------------------------------------------------
-BLS_HD fp fp_mul(const fp& a, const fp& b) {
+BLS_FN fp fp_mul(const fp& a, const fp& b) {
   fp r;
   uint32_t m[BLS_NL];
   uint64_t acc = 0;
@@ -71,7 +75,7 @@ BLS_HD fp fp_mul(const fp& a, const fp& b) {
   return r;
 }
 
-BLS_HD fp fp_sqr(const fp& a) {
+BLS_FN fp fp_sqr(const fp& a) {
   fp r;
   uint32_t m[BLS_NL];
   uint32_t a2[BLS_NL];

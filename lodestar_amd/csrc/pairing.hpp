@@ -10,7 +10,7 @@ struct g2proj {
 
 // Doubling step in homogeneous projective coordinates with the tangent line evaluated at P:
 //   line = (E - B) + (3 X^2 xP) v + (-H yP) v w
-BLS_HD void miller_dbl_step(g2proj& T, const fp& xP, const fp& yP, fp2& l0, fp2& l1, fp2& l4) {
+BLS_FN void miller_dbl_step(g2proj& T, const fp& xP, const fp& yP, fp2& l0, fp2& l1, fp2& l4) {
   fp2 A = fp2_half(fp2_mul(T.x, T.y));
   fp2 B = fp2_sqr(T.y);
   fp2 C = fp2_sqr(T.z);
@@ -32,7 +32,7 @@ BLS_HD void miller_dbl_step(g2proj& T, const fp& xP, const fp& yP, fp2& l0, fp2&
 
 // Mixed addition step T + Q (Q affine) with the chord line evaluated at P:
 //   line = (theta x2 - lambda y2) + (-theta xP) v + (lambda yP) v w
-BLS_HD void miller_add_step(g2proj& T, const g2a& Q, const fp& xP, const fp& yP, fp2& l0, fp2& l1, fp2& l4) {
+BLS_FN void miller_add_step(g2proj& T, const g2a& Q, const fp& xP, const fp& yP, fp2& l0, fp2& l1, fp2& l4) {
   fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
   fp2 lam = fp2_sub(T.x, fp2_mul(Q.x, T.z));
   fp2 C = fp2_sqr(theta);

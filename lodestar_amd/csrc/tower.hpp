@@ -19,43 +19,43 @@ BLS_HD fp2 fp2_make(const fp& a, const fp& b) {
 }
 BLS_HD fp2 fp2_zero() { return fp2_make(fp_zero(), fp_zero()); }
 BLS_HD fp2 fp2_one() { return fp2_make(FP_ONE, fp_zero()); }
-BLS_HD fp2 fp2_add(const fp2& a, const fp2& b) { return fp2_make(fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)); }
-BLS_HD fp2 fp2_sub(const fp2& a, const fp2& b) { return fp2_make(fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)); }
+BLS_FN fp2 fp2_add(const fp2& a, const fp2& b) { return fp2_make(fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)); }
+BLS_FN fp2 fp2_sub(const fp2& a, const fp2& b) { return fp2_make(fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)); }
 BLS_HD fp2 fp2_neg(const fp2& a) { return fp2_make(fp_neg(a.c0), fp_neg(a.c1)); }
 BLS_HD fp2 fp2_dbl(const fp2& a) { return fp2_make(fp_dbl(a.c0), fp_dbl(a.c1)); }
 BLS_HD fp2 fp2_half(const fp2& a) { return fp2_make(fp_half(a.c0), fp_half(a.c1)); }
 BLS_HD fp2 fp2_conj(const fp2& a) { return fp2_make(a.c0, fp_neg(a.c1)); }
 BLS_HD fp2 fp2_add_nr(const fp2& a, const fp2& b) { return fp2_make(fp_add_nr(a.c0, b.c0), fp_add_nr(a.c1, b.c1)); }
 
-BLS_HD fp2 fp2_mul(const fp2& a, const fp2& b) {
+BLS_FN fp2 fp2_mul(const fp2& a, const fp2& b) {
   fp t0 = fp_mul(a.c0, b.c0);
   fp t1 = fp_mul(a.c1, b.c1);
   fp t2 = fp_mul(fp_add_nr(a.c0, a.c1), fp_add_nr(b.c0, b.c1));
   return fp2_make(fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1));
 }
 
-BLS_HD fp2 fp2_sqr(const fp2& a) {
+BLS_FN fp2 fp2_sqr(const fp2& a) {
   fp c0 = fp_mul(fp_add_nr(a.c0, a.c1), fp_sub(a.c0, a.c1));
   fp c1 = fp_mul(fp_add_nr(a.c0, a.c0), a.c1);
   return fp2_make(c0, c1);
 }
 
-BLS_HD fp2 fp2_mul_fp(const fp2& a, const fp& s) { return fp2_make(fp_mul(a.c0, s), fp_mul(a.c1, s)); }
+BLS_FN fp2 fp2_mul_fp(const fp2& a, const fp& s) { return fp2_make(fp_mul(a.c0, s), fp_mul(a.c1, s)); }
 
 // (a0 + a1 u)(1 + u) = (a0 - a1) + (a0 + a1) u
-BLS_HD fp2 fp2_mul_xi(const fp2& a) { return fp2_make(fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)); }
+BLS_FN fp2 fp2_mul_xi(const fp2& a) { return fp2_make(fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)); }
 
-BLS_HD fp2 fp2_mul3(const fp2& a) { return fp2_make(fp_mul3(a.c0), fp_mul3(a.c1)); }
+BLS_FN fp2 fp2_mul3(const fp2& a) { return fp2_make(fp_mul3(a.c0), fp_mul3(a.c1)); }
 
-BLS_HD bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
-BLS_HD bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+BLS_FN bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+BLS_FN bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
 BLS_HD fp2 fp2_select(bool c, const fp2& a, const fp2& b) {
   return fp2_make(fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1));
 }
-BLS_HD fp fp2_norm(const fp2& a) {  // a0^2 + a1^2
+BLS_FN fp fp2_norm(const fp2& a) {  // a0^2 + a1^2
   return fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
 }
-BLS_HD fp2 fp2_inv(const fp2& a) {
+BLS_FN fp2 fp2_inv(const fp2& a) {
   fp ni = fp_inv(fp2_norm(a));
   return fp2_make(fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni)));
 }
@@ -101,12 +101,12 @@ BLS_HD fp6 fp6_make(const fp2& a, const fp2& b, const fp2& c) {
 }
 BLS_HD fp6 fp6_zero() { return fp6_make(fp2_zero(), fp2_zero(), fp2_zero()); }
 BLS_HD fp6 fp6_one() { return fp6_make(fp2_one(), fp2_zero(), fp2_zero()); }
-BLS_HD fp6 fp6_add(const fp6& a, const fp6& b) { return fp6_make(fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)); }
-BLS_HD fp6 fp6_sub(const fp6& a, const fp6& b) { return fp6_make(fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)); }
-BLS_HD fp6 fp6_neg(const fp6& a) { return fp6_make(fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)); }
-BLS_HD fp6 fp6_mul_v(const fp6& a) { return fp6_make(fp2_mul_xi(a.c2), a.c0, a.c1); }
+BLS_FN fp6 fp6_add(const fp6& a, const fp6& b) { return fp6_make(fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)); }
+BLS_FN fp6 fp6_sub(const fp6& a, const fp6& b) { return fp6_make(fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)); }
+BLS_FN fp6 fp6_neg(const fp6& a) { return fp6_make(fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)); }
+BLS_FN fp6 fp6_mul_v(const fp6& a) { return fp6_make(fp2_mul_xi(a.c2), a.c0, a.c1); }
 
-BLS_HD fp6 fp6_mul(const fp6& a, const fp6& b) {
+BLS_FN fp6 fp6_mul(const fp6& a, const fp6& b) {
   fp2 t0 = fp2_mul(a.c0, b.c0);
   fp2 t1 = fp2_mul(a.c1, b.c1);
   fp2 t2 = fp2_mul(a.c2, b.c2);
@@ -117,7 +117,7 @@ BLS_HD fp6 fp6_mul(const fp6& a, const fp6& b) {
 }
 
 // (x0 + x1 v + x2 v^2)(l0 + l1 v)
-BLS_HD fp6 fp6_mul_by_01(const fp6& x, const fp2& l0, const fp2& l1) {
+BLS_FN fp6 fp6_mul_by_01(const fp6& x, const fp2& l0, const fp2& l1) {
   fp2 t0 = fp2_mul(x.c0, l0);
   fp2 t1 = fp2_mul(x.c1, l1);
   fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(x.c2, l1)));
@@ -127,11 +127,11 @@ BLS_HD fp6 fp6_mul_by_01(const fp6& x, const fp2& l0, const fp2& l1) {
 }
 
 // (x0 + x1 v + x2 v^2) * (l1 v)
-BLS_HD fp6 fp6_mul_by_1(const fp6& x, const fp2& l1) {
+BLS_FN fp6 fp6_mul_by_1(const fp6& x, const fp2& l1) {
   return fp6_make(fp2_mul_xi(fp2_mul(x.c2, l1)), fp2_mul(x.c0, l1), fp2_mul(x.c1, l1));
 }
 
-BLS_HD fp6 fp6_inv(const fp6& a) {
+BLS_FN fp6 fp6_inv(const fp6& a) {
   fp2 t0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
   fp2 t1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
   fp2 t2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
@@ -149,7 +149,7 @@ BLS_HD fp12 fp12_make(const fp6& a, const fp6& b) {
 }
 BLS_HD fp12 fp12_one() { return fp12_make(fp6_one(), fp6_zero()); }
 
-BLS_HD fp12 fp12_mul(const fp12& a, const fp12& b) {
+BLS_FN fp12 fp12_mul(const fp12& a, const fp12& b) {
   fp6 t0 = fp6_mul(a.c0, b.c0);
   fp6 t1 = fp6_mul(a.c1, b.c1);
   fp6 c1 = fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), fp6_add(t0, t1));
@@ -158,7 +158,7 @@ BLS_HD fp12 fp12_mul(const fp12& a, const fp12& b) {
 }
 
 // (a0 + a1 w)^2 = (a0^2 + v a1^2) + 2 a0 a1 w ;  complex-method squaring, 2 Fp6 muls
-BLS_HD fp12 fp12_sqr(const fp12& a) {
+BLS_FN fp12 fp12_sqr(const fp12& a) {
   fp6 t = fp6_mul(a.c0, a.c1);
   fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
   fp6 c0 = fp6_sub(fp6_sub(s, t), fp6_mul_v(t));
@@ -168,14 +168,14 @@ BLS_HD fp12 fp12_sqr(const fp12& a) {
 
 BLS_HD fp12 fp12_conj(const fp12& a) { return fp12_make(a.c0, fp6_neg(a.c1)); }
 
-BLS_HD fp12 fp12_inv(const fp12& a) {
+BLS_FN fp12 fp12_inv(const fp12& a) {
   fp6 t = fp6_sub(fp6_mul(a.c0, a.c0), fp6_mul_v(fp6_mul(a.c1, a.c1)));
   fp6 ti = fp6_inv(t);
   return fp12_make(fp6_mul(a.c0, ti), fp6_neg(fp6_mul(a.c1, ti)));
 }
 
 // f * line, line = l0 + l1 v + l4 v w   (positions c0.c0, c0.c1, c1.c1) -- 13 Fp2 multiplications
-BLS_HD fp12 fp12_mul_by_014(const fp12& f, const fp2& l0, const fp2& l1, const fp2& l4) {
+BLS_FN fp12 fp12_mul_by_014(const fp12& f, const fp2& l0, const fp2& l1, const fp2& l4) {
   fp6 a0 = fp6_mul_by_01(f.c0, l0, l1);
   fp6 a1 = fp6_mul_by_1(f.c1, l4);
   fp6 s = fp6_mul_by_01(fp6_add(f.c0, f.c1), l0, fp2_add(l1, l4));
@@ -185,7 +185,7 @@ BLS_HD fp12 fp12_mul_by_014(const fp12& f, const fp2& l0, const fp2& l1, const f
 }
 
 // Frobenius x -> x^(p^k) for k = 1, 2, 3
-BLS_HD fp12 fp12_frob1(const fp12& a) {
+BLS_FN fp12 fp12_frob1(const fp12& a) {
   fp12 r;
   r.c0.c0 = fp2_conj(a.c0.c0);
   r.c1.c0 = fp2_mul(fp2_conj(a.c1.c0), FROB1_1);
@@ -195,7 +195,7 @@ BLS_HD fp12 fp12_frob1(const fp12& a) {
   r.c1.c2 = fp2_mul(fp2_conj(a.c1.c2), FROB1_5);
   return r;
 }
-BLS_HD fp12 fp12_frob2(const fp12& a) {
+BLS_FN fp12 fp12_frob2(const fp12& a) {
   fp12 r;
   r.c0.c0 = a.c0.c0;
   r.c1.c0 = fp2_mul(a.c1.c0, FROB2_1);
@@ -206,7 +206,7 @@ BLS_HD fp12 fp12_frob2(const fp12& a) {
   return r;
 }
 
-BLS_HD bool fp12_is_one(const fp12& a) {
+BLS_FN bool fp12_is_one(const fp12& a) {
   bool r = fp2_eq(a.c0.c0, fp2_one());
   r = r && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2);
   r = r && fp2_is_zero(a.c1.c0) && fp2_is_zero(a.c1.c1) && fp2_is_zero(a.c1.c2);

@@ -1,0 +1,209 @@
+"""ctypes binding of libblsgpu.so (include/blsgpu.h).  Loads the in-tree library and fails loudly if it
+is missing -- there is no CPU fallback for verification."""
+import ctypes
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libblsgpu.so")
+
+# job / status codes (blsgpu_code)
+OK = 0
+BAD_ENCODING = 1
+POINT_NOT_ON_CURVE = 2
+POINT_NOT_IN_GROUP = 3
+PK_IS_INFINITY = 6
+INVALID_SIZE = 8
+EMPTY_AGGREGATE = 9
+EMPTY_SET = 10
+DEVICE_ERROR = 11
+ERR_ARGS = 100
+ERR_NO_DEVICE = 101
+ERR_CLOSED = 102
+
+EXPORTED_SYMBOLS = [
+    "blsgpu_init",
+    "blsgpu_destroy",
+    "blsgpu_device_count",
+    "blsgpu_pubkeys_upload",
+    "blsgpu_pubkeys_count",
+    "blsgpu_verify",
+    "blsgpu_submit",
+    "blsgpu_set_option",
+    "blsgpu_code_name",
+    "blsgpu_debug_op",
+]
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [
+        ("n_sets", ctypes.c_uint32),
+        ("n_jobs", ctypes.c_uint32),
+        ("job_first_set", ctypes.c_void_p),
+        ("job_flags", ctypes.c_void_p),
+        ("pk_bytes", ctypes.c_void_p),
+        ("set_pk_first", ctypes.c_void_p),
+        ("pk_index", ctypes.c_void_p),
+        ("msgs", ctypes.c_void_p),
+        ("sigs", ctypes.c_void_p),
+        ("sig_len", ctypes.c_void_p),
+        ("sig_stride", ctypes.c_uint32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("groups", ctypes.c_uint32),
+        ("batch_retries", ctypes.c_uint32),
+        ("batch_sigs_success", ctypes.c_uint32),
+        ("devices_used", ctypes.c_uint32),
+        ("device_ms", ctypes.c_double),
+    ]
+
+
+DONE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `python -m lodestar_amd.build` (hipcc, gfx950). "
+            "There is no CPU verification path."
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.blsgpu_init.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    lib.blsgpu_init.restype = ctypes.c_int
+    lib.blsgpu_destroy.argtypes = [ctypes.c_void_p]
+    lib.blsgpu_destroy.restype = None
+    lib.blsgpu_device_count.argtypes = [ctypes.c_void_p]
+    lib.blsgpu_device_count.restype = ctypes.c_int
+    lib.blsgpu_pubkeys_upload.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]
+    lib.blsgpu_pubkeys_upload.restype = ctypes.c_int
+    lib.blsgpu_pubkeys_count.argtypes = [ctypes.c_void_p]
+    lib.blsgpu_pubkeys_count.restype = ctypes.c_uint32
+    lib.blsgpu_verify.argtypes = [ctypes.c_void_p, ctypes.POINTER(Batch), ctypes.c_void_p, ctypes.POINTER(Stats)]
+    lib.blsgpu_verify.restype = ctypes.c_int
+    lib.blsgpu_submit.argtypes = [ctypes.c_void_p, ctypes.POINTER(Batch), ctypes.c_void_p, ctypes.POINTER(Stats),
+                                  DONE_CB, ctypes.c_void_p]
+    lib.blsgpu_submit.restype = ctypes.c_int
+    lib.blsgpu_set_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]
+    lib.blsgpu_set_option.restype = ctypes.c_int
+    lib.blsgpu_code_name.argtypes = [ctypes.c_int]
+    lib.blsgpu_code_name.restype = ctypes.c_char_p
+    lib.blsgpu_debug_op.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                    ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    lib.blsgpu_debug_op.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def code_name(code: int) -> str:
+    n = load().blsgpu_code_name(code)
+    return n.decode() if n else f"BLSGPU_{code}"
+
+
+class Context:
+    """Owns a blsgpu_ctx on one or more HIP devices."""
+
+    def __init__(self, devices=None):
+        lib = load()
+        self._lib = lib
+        h = ctypes.c_void_p()
+        if devices:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = lib.blsgpu_init(arr, len(devices), ctypes.byref(h))
+        else:
+            rc = lib.blsgpu_init(None, 0, ctypes.byref(h))
+        if rc != OK:
+            raise RuntimeError(f"blsgpu_init failed: {code_name(rc)} (no usable MI355X?)")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self._lib.blsgpu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def device_count(self):
+        return self._lib.blsgpu_device_count(self.h)
+
+    def set_option(self, key: str, value: int):
+        rc = self._lib.blsgpu_set_option(self.h, key.encode(), int(value))
+        if rc != OK:
+            raise ValueError(f"blsgpu_set_option({key}) -> {code_name(rc)}")
+
+    def upload_pubkeys(self, first_index: int, pk96: bytes):
+        n = len(pk96) // 96
+        rc = self._lib.blsgpu_pubkeys_upload(self.h, first_index, pk96, n)
+        if rc != OK:
+            raise ValueError(f"blsgpu_pubkeys_upload -> {code_name(rc)}")
+
+    @property
+    def pubkeys_count(self):
+        return self._lib.blsgpu_pubkeys_count(self.h)
+
+    def verify_raw(self, job_first_set, sigs, sig_len, msgs, pk_bytes=None, set_pk_first=None, pk_index=None,
+                   job_flags=None, sig_stride=None, seed=0x4C4F444553544152):
+        """Low-level call: numpy/bytes arrays in, (job_result int8 array, Stats) out."""
+        job_first_set = np.ascontiguousarray(job_first_set, dtype=np.uint32)
+        n_jobs = len(job_first_set) - 1
+        sig_len = np.ascontiguousarray(sig_len, dtype=np.uint32)
+        n_sets = len(sig_len)
+        if sig_stride is None:
+            sig_stride = (len(sigs) // n_sets) if n_sets else 96
+        sigs = np.frombuffer(bytes(sigs), dtype=np.uint8) if not isinstance(sigs, np.ndarray) else sigs
+        msgs = np.frombuffer(bytes(msgs), dtype=np.uint8) if not isinstance(msgs, np.ndarray) else msgs
+        keep = [job_first_set, sig_len, sigs, msgs]
+        b = Batch()
+        b.n_sets = n_sets
+        b.n_jobs = n_jobs
+        b.job_first_set = job_first_set.ctypes.data
+        if job_flags is not None:
+            job_flags = np.ascontiguousarray(job_flags, dtype=np.uint8)
+            keep.append(job_flags)
+            b.job_flags = job_flags.ctypes.data
+        if pk_bytes is not None:
+            pk = np.frombuffer(bytes(pk_bytes), dtype=np.uint8) if not isinstance(pk_bytes, np.ndarray) else pk_bytes
+            keep.append(pk)
+            b.pk_bytes = pk.ctypes.data
+        else:
+            set_pk_first = np.ascontiguousarray(set_pk_first, dtype=np.uint32)
+            pk_index = np.ascontiguousarray(pk_index, dtype=np.uint32)
+            keep += [set_pk_first, pk_index]
+            b.set_pk_first = set_pk_first.ctypes.data
+            b.pk_index = pk_index.ctypes.data if len(pk_index) else set_pk_first.ctypes.data
+        b.msgs = msgs.ctypes.data
+        b.sigs = sigs.ctypes.data
+        b.sig_len = sig_len.ctypes.data
+        b.sig_stride = sig_stride
+        b.seed = seed
+        res = np.zeros(max(n_jobs, 1), dtype=np.int8)
+        st = Stats()
+        rc = self._lib.blsgpu_verify(self.h, ctypes.byref(b), res.ctypes.data, ctypes.byref(st))
+        if rc != OK:
+            raise RuntimeError(f"blsgpu_verify -> {code_name(rc)}")
+        return res[:n_jobs], st
+
+    def debug_op(self, op: int, inputs: bytes, in_stride: int, out_stride: int):
+        n = len(inputs) // in_stride
+        inb = np.frombuffer(inputs, dtype=np.uint8).copy()
+        out = np.zeros(n * out_stride, dtype=np.uint8)
+        st = np.zeros(n, dtype=np.int32)
+        rc = self._lib.blsgpu_debug_op(self.h, op, n, inb.ctypes.data, in_stride, out.ctypes.data, out_stride,
+                                       st.ctypes.data)
+        if rc != OK:
+            raise RuntimeError(f"blsgpu_debug_op -> {code_name(rc)}")
+        return out.tobytes(), st

@@ -1,0 +1,207 @@
+"""GPU parity tests: every stage of the HIP pipeline and the C-ABI verify path against the oracle.
+Run on the MI355X box:  python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread"""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+from oracle import bls12_381 as bls
+from tests.emu_helpers import b2f12, b2g1, b2g2, f12b, fpb, fromb, g1b, g2b
+
+pytestmark = pytest.mark.gpu
+
+P = bls.P
+SEED = 0x4C4F444553544152
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from lodestar_amd.native import Context
+
+    c = Context()
+    yield c
+    c.close()
+
+
+def msg_j(j, seed=SEED):
+    return hashlib.sha256(seed.to_bytes(8, "little") + j.to_bytes(4, "little")).digest()
+
+
+def test_debug_fp_mul(ctx):
+    rnd = random.Random(7)
+    pairs = [(rnd.randrange(P), rnd.randrange(P)) for _ in range(200)] + [(P - 1, P - 1), (0, 5), (1, P - 1)]
+    inp = b"".join(fpb(a) + fpb(b) for a, b in pairs)
+    out, st = ctx.debug_op(0, inp, 96, 48)
+    for k, (a, b) in enumerate(pairs):
+        assert fromb(out[48 * k : 48 * k + 48]) == a * b % P
+
+
+def test_debug_sig_decode(ctx):
+    sig = bls.sign(0x1234567, b"\x07" * 32)
+    cases = [bls.g2_compress(sig), bls.g2_serialize(sig), bytes(32), bytes([0xC0]) + bytes(95),
+             bytes([0xE0]) + bytes(95), bytes([0x9A]) + b"\xff" * 95]
+    for t in range(1, 30):
+        cases.append(bytes([0x80]) + bytes(46) + bytes([t]) + bytes(48))
+    inp = b""
+    for c in cases:
+        rec = c.ljust(192, b"\x00") + len(c).to_bytes(2, "little")
+        inp += rec
+    out, st = ctx.debug_op(1, inp, 194, 192)
+    for k, c in enumerate(cases):
+        want = bls.classify_signature(c)
+        got = int(st[k])
+        if got == -1:  # infinity
+            assert bls.signature_from_bytes(c) is None
+            continue
+        assert got == want, (k, c.hex()[:20], got, want)
+        if want == 0:
+            assert b2g2(out[192 * k : 192 * k + 192]) == bls.signature_from_bytes(c)
+
+
+def test_debug_hash_to_g2(ctx):
+    msgs = [msg_j(j) for j in range(64)] + [bytes(32), b"\xff" * 32]
+    out, st = ctx.debug_op(2, b"".join(msgs), 32, 192)
+    for k, m in enumerate(msgs[:12] + msgs[-2:]):
+        idx = msgs.index(m)
+        assert st[idx] == 0
+        assert b2g2(out[192 * idx : 192 * idx + 192]) == bls.hash_to_g2(m)
+
+
+def test_debug_miller_final_exp(ctx):
+    rnd = random.Random(3)
+    pts = [(bls.g1_mul(bls.G1_GEN, rnd.randrange(1, bls.R)), bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R)))
+           for _ in range(3)]
+    inp = b"".join(g1b(p) + g2b(q) for p, q in pts)
+    out, st = ctx.debug_op(3, inp, 288, 576)
+    fs = []
+    for k, (p, q) in enumerate(pts):
+        f = b2f12(out[576 * k : 576 * k + 576])
+        assert f == bls.miller_loop(p, q)
+        fs.append(f)
+    out2, _ = ctx.debug_op(4, b"".join(f12b(f) for f in fs), 576, 576)
+    for k, f in enumerate(fs):
+        assert b2f12(out2[576 * k : 576 * k + 576]) == bls.final_exp(f)
+
+
+def test_debug_scalar_mul(ctx):
+    rnd = random.Random(11)
+    Pp = bls.g1_mul(bls.G1_GEN, 99)
+    Q = bls.g2_mul(bls.G2_GEN, 77)
+    ks = [1, 2, 3, 0xFFFFFFFFFFFFFFFF] + [rnd.getrandbits(64) for _ in range(12)]
+    out, st = ctx.debug_op(5, b"".join(g1b(Pp) + k.to_bytes(8, "little") for k in ks), 104, 96)
+    for i, k in enumerate(ks):
+        assert b2g1(out[96 * i : 96 * i + 96]) == bls.g1_mul(Pp, k)
+    out, st = ctx.debug_op(6, b"".join(g2b(Q) + k.to_bytes(8, "little") for k in ks[:6]), 200, 192)
+    for i, k in enumerate(ks[:6]):
+        assert b2g2(out[192 * i : 192 * i + 192]) == bls.g2_mul(Q, k)
+
+
+# ---------------------------------------------------------------------------- verify (C-ABI)
+def make_sets(n, seed=SEED, start=0):
+    out = []
+    for j in range(start, start + n):
+        sk = bls.interop_secret_key(j)
+        m = msg_j(j, seed)
+        pk = bls.sk_to_pk(sk)
+        out.append((sk, pk, m, bls.g2_compress(bls.sign(sk, m))))
+    return out
+
+
+@pytest.fixture(scope="module")
+def sets16():
+    return make_sets(16)
+
+
+def run_bytes_mode(ctx, sets, jobs, batchable=None, sigs_override=None, **kw):
+    jfs = [0]
+    for j in jobs:
+        jfs.append(jfs[-1] + j)
+    assert jfs[-1] == len(sets)
+    sig_list = sigs_override or [s[3] for s in sets]
+    stride = 192
+    sigs = b"".join(s.ljust(stride, b"\x00")[:stride] for s in sig_list)
+    sig_len = [len(s) for s in sig_list]
+    msgs = b"".join(s[2] for s in sets)
+    pkb = b"".join(bls.g1_serialize(s[1]) for s in sets)
+    flags = None if batchable is None else [1 if b else 0 for b in batchable]
+    return ctx.verify_raw(jfs, sigs, sig_len, msgs, pk_bytes=pkb, job_flags=flags, sig_stride=stride, **kw)
+
+
+def test_verify_single_and_batch(ctx, sets16):
+    res, st = run_bytes_mode(ctx, sets16, [1] * 16)
+    assert list(res) == [1] * 16
+    res, st = run_bytes_mode(ctx, sets16, [16])
+    assert list(res) == [1]
+    res, st = run_bytes_mode(ctx, sets16, [1] * 16, batchable=[True] * 16)
+    assert list(res) == [1] * 16
+    assert st.groups == 1 and st.batch_retries == 0
+
+
+def test_verify_invalid_isolation(ctx, sets16):
+    """multithread.test.ts:89-106: an invalid job does not make the others fail."""
+    sigs = [s[3] for s in sets16]
+    sigs[0] = bytes(32)  # BLST_INVALID_SIZE
+    sigs[5] = sets16[6][3]  # well-formed, wrong signature -> false
+    res, st = run_bytes_mode(ctx, sets16, [1] * 16, batchable=[True] * 16, sigs_override=sigs)
+    want = [-8] + [1] * 4 + [0] + [1] * 10
+    assert list(res) == want
+    assert st.batch_retries == 1
+    # non-batchable multi-set job containing the wrong signature -> false, others true
+    res, st = run_bytes_mode(ctx, sets16, [4, 4, 8], sigs_override=[s[3] for s in sets16[:5]] + [sets16[6][3]] + [s[3] for s in sets16[6:]])
+    assert list(res) == [1, 0, 1]
+
+
+def test_verify_error_classes(ctx, sets16):
+    sigs = [s[3] for s in sets16]
+    sigs[1] = bytes([0xC0]) + bytes(95)  # infinity -> false
+    sigs[2] = bytes([0xE0]) + bytes(95)  # bad encoding
+    x = None
+    for t in range(1, 60):
+        cand = bytes([0x80]) + bytes(46) + bytes([t]) + bytes(48)
+        c = bls.classify_signature(cand)
+        if c == bls.BLST_POINT_NOT_ON_CURVE and x is None:
+            x = cand
+        if c == bls.BLST_POINT_NOT_IN_GROUP:
+            sigs[4] = cand
+    sigs[3] = x
+    sigs[6] = bls.g2_serialize(bls.signature_from_bytes(sets16[6][3]))  # 192-byte form, valid
+    res, _ = run_bytes_mode(ctx, sets16, [1] * 16, batchable=[True] * 16, sigs_override=sigs)
+    assert list(res[:7]) == [1, 0, -1, -2, -3, 1, 1]
+    assert all(r == 1 for r in res[7:])
+
+
+def test_verify_empty_job(ctx, sets16):
+    res, _ = run_bytes_mode(ctx, sets16[:2], [0, 2, 0])
+    assert list(res) == [-10, 1, -10]
+
+
+def test_verify_table_mode_aggregate(ctx):
+    n_keys = 40
+    sks = [bls.interop_secret_key(i) for i in range(n_keys)]
+    pks = [bls.sk_to_pk(s) for s in sks]
+    ctx.upload_pubkeys(0, b"".join(bls.g1_serialize(p) for p in pks))
+    assert ctx.pubkeys_count >= n_keys
+    # aggregate sets: same message signed by several keys; aggregate signature = (sum sk) H(m)
+    groups = [list(range(0, 7)), list(range(7, 8)), list(range(8, 40)), [3, 3, 5]]
+    sets = []
+    for gi, g in enumerate(groups):
+        m = msg_j(1000 + gi)
+        sk_sum = sum(sks[i] for i in g) % bls.R
+        sig = bls.g2_compress(bls.sign(sk_sum, m))
+        sets.append((g, m, sig))
+    jfs = list(range(len(sets) + 1))
+    set_pk_first = [0]
+    pk_index = []
+    for g, _, _ in sets:
+        pk_index += g
+        set_pk_first.append(len(pk_index))
+    sigs = b"".join(s[2] for s in sets)
+    msgs = b"".join(s[1] for s in sets)
+    res, _ = ctx.verify_raw(jfs, sigs, [96] * len(sets), msgs, set_pk_first=set_pk_first, pk_index=pk_index,
+                            sig_stride=96)
+    assert list(res) == [1, 1, 1, 1]
+    # empty aggregate -> EMPTY_AGGREGATE_ARRAY
+    res, _ = ctx.verify_raw([0, 1, 2], sigs[:192], [96, 96], msgs[:64], set_pk_first=[0, 7, 7],
+                            pk_index=list(range(7)), sig_stride=96)
+    assert list(res) == [1, -9]
