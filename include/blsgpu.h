@@ -77,6 +77,10 @@ typedef struct blsgpu_stats {
   uint32_t batch_sigs_success; /* sets accepted by a batch group (metric blsThreadPool.batchSigsSuccess) */
   uint32_t devices_used;
   double device_ms; /* wall time of the device phase (max over devices) */
+  /* With option "profile" = 1: per-stage kernel time (HIP events on the launch stream, device 0 shard):
+   * 0 sig_decode 1 hash_to_g2 2 pk_aggregate 3 pk_finish 4 sig_scale 5 miller_sets
+   * 6 group_sig_miller 7 group_finish */
+  double stage_ms[8];
 } blsgpu_stats;
 
 /* Create a context on the given HIP devices (NULL / n <= 0: every visible device). */
@@ -101,7 +105,7 @@ typedef void (*blsgpu_done_cb)(void* user, int status);
 int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result, blsgpu_stats* stats,
                   blsgpu_done_cb done, void* user);
 
-/* Tunables: "group_sets" (target sets per batch group, default 64), "max_devices". */
+/* Tunables: "group_sets" (target sets per batch group, default 64), "max_devices", "profile" (0/1). */
 int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value);
 
 /* "BLST_INVALID_SIZE", ... for job codes; NULL for unknown codes. */
@@ -110,6 +114,7 @@ const char* blsgpu_code_name(int code);
 /* Test hook: run one pipeline stage element-wise on device 0 (canonical big-endian encodings).
  * op: 0 fp_mul(48,48->48) 1 sig_decode(192+len -> status,192) 2 hash_to_g2(32->192)
  *     3 miller(96,192->576) 4 final_exp(576->576) 5 g1_mul_u64(96,8->96) 6 g2_mul_u64(192,8->192)
+ *     7 sign(sk32||msg32 -> 96 compressed) 8 sk_to_pk(sk32 -> 96 uncompressed)   (workload generation)
  * Returns BLSGPU_OK or an error. */
 int blsgpu_debug_op(blsgpu_ctx* ctx, int op, uint32_t n, const uint8_t* in, uint32_t in_stride,
                     uint8_t* out, uint32_t out_stride, int32_t* status);

@@ -43,10 +43,20 @@ struct fp2 {
 
 #include "bls_constants.hpp"
 
+// Host-only instrumentation (tests/native/emu.cpp with -DBLS_COUNT_OPS): counts Montgomery
+// multiplications / squarings of the device algorithm to give the roofline its algorithmic work.
+#if defined(BLS_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
+extern unsigned long long bls_count_mul, bls_count_sqr;
+#define BLS_COUNT(x) (x++)
+#else
+#define BLS_COUNT(x) ((void)0)
+#endif
+
 // ------------------------------------------------------------------------------------------------
 // Montgomery multiplication: finely integrated product scanning (column-wise a*b and m*p).
 // ------------------------------------------------------------------------------------------------
 BLS_FN fp fp_mul(const fp& a, const fp& b) {
+  BLS_COUNT(bls_count_mul);
   fp r;
   uint32_t m[BLS_NL];
   uint64_t acc = 0;
@@ -76,6 +86,7 @@ BLS_FN fp fp_mul(const fp& a, const fp& b) {
 }
 
 BLS_FN fp fp_sqr(const fp& a) {
+  BLS_COUNT(bls_count_sqr);
   fp r;
   uint32_t m[BLS_NL];
   uint32_t a2[BLS_NL];

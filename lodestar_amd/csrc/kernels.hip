@@ -130,6 +130,17 @@ __device__ jac<F> jac_mul_u64_j(const jac<F>& P, uint64_t k) {
   return r;
 }
 
+// [k]P for a multi-word scalar (little-endian 32-bit words), used by the workload-generation ops
+template <class F>
+__device__ jac<F> jac_mul_words(const jac<F>& P, const uint32_t* k, int nw) {
+  jac<F> r = jac_infinity<F>();
+  for (int i = 32 * nw - 1; i >= 0; i--) {
+    r = jac_dbl(r);
+    if ((k[i >> 5] >> (i & 31)) & 1u) r = jac_add(r, P);
+  }
+  return r;
+}
+
 // ------------------------------------------------------------------------------------------ kernels
 __global__ __launch_bounds__(WAVE) void k_sig_decode(PipelineBuffers b, uint32_t n_sets) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
@@ -415,6 +426,32 @@ __global__ __launch_bounds__(WAVE) void k_debug_op(int op, uint32_t n, const uin
       g2a r;
       st = jac_to_aff(jac_mul_u64(dbg_load_g2(a), k), r) ? 0 : -1;
       if (st == 0) g2a_to_be192(r, o);
+      break;
+    }
+    case 7: {  // sign: sk (32 B big-endian) || msg (32 B) -> compressed signature (96 B)
+      uint32_t w[8];
+      for (int j = 0; j < 8; j++)
+        w[j] = ((uint32_t)a[31 - 4 * j]) | ((uint32_t)a[30 - 4 * j] << 8) | ((uint32_t)a[29 - 4 * j] << 16) |
+               ((uint32_t)a[28 - 4 * j] << 24);
+      g2j h = hash_to_g2_jac(a + 32);
+      g2a ha;
+      st = jac_to_aff(h, ha) ? 0 : -1;
+      g2a s;
+      if (st == 0) st = jac_to_aff(jac_mul_words(jac_from_aff(ha), w, 8), s) ? 0 : -1;
+      if (st == 0) g2a_compress(s, o);
+      break;
+    }
+    case 8: {  // sk_to_pk: sk (32 B big-endian) -> uncompressed pubkey (96 B)
+      uint32_t w[8];
+      for (int j = 0; j < 8; j++)
+        w[j] = ((uint32_t)a[31 - 4 * j]) | ((uint32_t)a[30 - 4 * j] << 8) | ((uint32_t)a[29 - 4 * j] << 16) |
+               ((uint32_t)a[28 - 4 * j] << 24);
+      g1a g;
+      g.x = G1_GEN_X;
+      g.y = G1_GEN_Y;
+      g1a pk;
+      st = jac_to_aff(jac_mul_words(jac_from_aff(g), w, 8), pk) ? 0 : -1;
+      if (st == 0) g1a_to_be96(pk, o);
       break;
     }
     default:

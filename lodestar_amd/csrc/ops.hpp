@@ -111,3 +111,13 @@ BLS_HD void g1a_to_be96(const g1a& p, uint8_t* b) {
   fp_to_be48(p.x, b);
   fp_to_be48(p.y, b + 48);
 }
+
+// ZCash compressed encoding of an affine G2 point (not infinity)
+BLS_HD void g2a_compress(const g2a& p, uint8_t* b) {
+  fp_to_be48(p.x.c1, b);
+  fp_to_be48(p.x.c0, b + 48);
+  fp2 yp = fp2_plain(p.y);
+  bool c1z = fp_is_zero(yp.c1);
+  bool largest = c1z ? fp_plain_gt_half(yp.c0) : fp_plain_gt_half(yp.c1);
+  b[0] |= 0x80 | (largest ? 0x20 : 0);
+}

@@ -125,6 +125,7 @@ struct blsgpu_ctx {
   std::mutex table_mu;
   int64_t group_sets = 64;
   int64_t max_devices = 64;
+  bool profile = false;
 };
 
 namespace {
@@ -274,14 +275,30 @@ int run_shard(blsgpu_ctx* ctx, Device& d, const blsgpu_batch& b, const Shard& sh
   pb.status = d.d_status.p;
 
   // ---- kernel pipeline ---------------------------------------------------------------------------
+  const bool prof = ctx->profile;
+  hipEvent_t ev[9];
+  if (prof)
+    for (int k = 0; k < 9; k++) HIPCHK(hipEventCreate(&ev[k]));
+  auto mark = [&](int k) {
+    if (prof) HIPCHK(hipEventRecord(ev[k], s));
+  };
+  mark(0);
   launch_sig_decode(pb, n, s);
+  mark(1);
   launch_hash_to_g2(pb, n, s);
+  mark(2);
   if (table_mode) launch_pk_aggregate(pb, n, s);
+  mark(3);
   launch_pk_finish(pb, n, s);
+  mark(4);
   launch_sig_scale(pb, n, s);
+  mark(5);
   launch_miller_sets(pb, n, s);
+  mark(6);
   launch_group_sig_miller(pb, d.d_groups.p, ng, d.d_fgroup.p, s);
+  mark(7);
   launch_group_finish(pb, d.d_groups.p, ng, d.d_fgroup.p, d.d_ok.p, s);
+  mark(8);
   HIPCHK(hipGetLastError());
   d.h_status.ensure((size_t)stride * 2);
   d.h_ok.ensure(std::max<uint32_t>(ng, nj) + 1);
@@ -289,6 +306,14 @@ int run_shard(blsgpu_ctx* ctx, Device& d, const blsgpu_batch& b, const Shard& sh
   if (ng) HIPCHK(hipMemcpyAsync(d.h_ok.p, d.d_ok.p, ng, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   st.groups += ng;
+  if (prof) {
+    for (int k = 0; k < 8; k++) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      st.stage_ms[k] += ms;
+    }
+    for (int k = 0; k < 9; k++) (void)hipEventDestroy(ev[k]);
+  }
 
   // ---- per-job results ---------------------------------------------------------------------------
   const int8_t* sig_st = d.h_status.p;
@@ -511,6 +536,8 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   if (k == "group_sets") {
     if (value < 1) return BLSGPU_ERR_ARGS;
     ctx->group_sets = value;
+  } else if (k == "profile") {
+    ctx->profile = value != 0;
   } else if (k == "max_devices") {
     if (value < 1) return BLSGPU_ERR_ARGS;
     ctx->max_devices = value;
@@ -581,6 +608,7 @@ int blsgpu_verify(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, bl
   }
   auto t1 = std::chrono::steady_clock::now();
   int status = BLSGPU_OK;
+  for (int k = 0; k < 8; k++) local.stage_ms[k] = sst[0].stage_ms[k];
   for (size_t k = 0; k < shards.size(); k++) {
     local.groups += sst[k].groups;
     local.batch_retries += sst[k].batch_retries;

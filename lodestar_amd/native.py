@@ -60,7 +60,14 @@ class Stats(ctypes.Structure):
         ("batch_sigs_success", ctypes.c_uint32),
         ("devices_used", ctypes.c_uint32),
         ("device_ms", ctypes.c_double),
+        ("stage_ms", ctypes.c_double * 8),
     ]
+
+
+STAGES = ["sig_decode", "hash_to_g2", "pk_aggregate", "pk_finish", "sig_scale", "miller_sets",
+          "group_sig_miller", "group_finish"]
+KERNEL_OF_STAGE = ["k_sig_decode", "k_hash_to_g2", "k_pk_aggregate", "k_pk_finish", "k_sig_scale",
+                   "k_miller_sets", "k_group_sig_miller", "k_group_finish"]
 
 
 DONE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)

@@ -4,6 +4,10 @@
 #include <string.h>
 #include "../../lodestar_amd/csrc/ops.hpp"
 
+#if defined(BLS_COUNT_OPS)
+unsigned long long bls_count_mul = 0, bls_count_sqr = 0;
+#endif
+
 static fp load_mont(const uint8_t* b) {
   fp x;
   fp_from_be48_plain(b, x, 0xff);
@@ -53,6 +57,43 @@ static fp12 load12(const uint8_t* b) {
 }
 
 extern "C" {
+#if defined(BLS_COUNT_OPS)
+void emu_count_reset() { bls_count_mul = bls_count_sqr = 0; }
+unsigned long long emu_count_mul() { return bls_count_mul; }
+unsigned long long emu_count_sqr() { return bls_count_sqr; }
+// kernel-shaped stages (same calls as kernels.hip)
+void emu_stage_sig_scale(const uint8_t* sig192, uint64_t r) { (void)jac_mul_u64(load_g2(sig192), r); }
+void emu_stage_pk_finish(const uint8_t* pk96, uint64_t r) {
+  g1a a;
+  (void)jac_to_aff(jac_mul_u64(load_g1(pk96), r), a);
+}
+void emu_stage_group_sig_miller(const uint8_t* sig192, int n) {
+  g2j S = jac_infinity<fp2>();
+  g2j s = jac_from_aff(load_g2(sig192));
+  g2j t = jac_dbl(s);
+  for (int i = 0; i < n; i++) S = jac_add(S, (i & 1) ? s : t);
+  g2a Sa;
+  jac_to_aff(S, Sa);
+  g1a ng;
+  ng.x = G1_GEN_X;
+  ng.y = G1_NEG_GEN_Y;
+  (void)miller_loop(ng, Sa);
+}
+void emu_stage_group_finish(const uint8_t* f576, int n) {
+  fp12 f = load12(f576);
+  fp12 acc = f;
+  for (int i = 0; i < n; i++) acc = fp12_mul(acc, f);
+  (void)final_exponentiation(acc);
+}
+void emu_stage_pk_aggregate(const uint8_t* pk96, int n) {
+  g1a p = load_g1(pk96);
+  g1j acc = jac_infinity<fp>();
+  g1j two = jac_dbl(jac_from_aff(p));
+  g1a p2;
+  jac_to_aff(two, p2);
+  for (int i = 0; i < n; i++) acc = jac_add_aff(acc, (i & 1) ? p : p2);
+}
+#endif
 void emu_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp_to_be48(fp_mul(load_mont(a), load_mont(b)), out); }
 void emu_fp_sqr(const uint8_t* a, uint8_t* out) { fp_to_be48(fp_sqr(load_mont(a)), out); }
 void emu_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp_to_be48(fp_add(load_mont(a), load_mont(b)), out); }
