@@ -6,6 +6,7 @@
 import os
 import subprocess
 import sys
+import time
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -13,7 +14,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libblsgpu.so")
 ARCH = os.environ.get("BLSGPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["kernels.hip", "runtime.cpp"]
+SOURCES = ["k_sig.hip", "k_hash.hip", "k_pk.hip", "k_miller.hip", "k_group.hip", "k_debug.hip", "runtime.cpp"]
 
 
 def _deps():
@@ -36,17 +37,21 @@ def build(force=False, verbose=True):
         return LIB
     objs = []
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include")]
+    # one translation unit per pipeline stage, compiled in parallel (the stage kernels are large)
     procs = []
+    t0 = time.time()
     for src in SOURCES:
         obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
         objs.append(obj)
         cmd = [HIPCC] + common + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
-        procs.append(subprocess.Popen(cmd))
-    for p in procs:
+        procs.append((src, subprocess.Popen(cmd)))
+    for src, p in procs:
         if p.wait() != 0:
-            raise RuntimeError("hipcc failed")
+            raise RuntimeError(f"hipcc failed on {src}")
+        if verbose:
+            print(f"  {src}: done at {time.time() - t0:.0f} s", flush=True)
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", LIB] + objs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)

@@ -89,7 +89,7 @@ BLS_HD jac<F> jac_neg(const jac<F>& p) {
 
 // p + q with q affine (q never infinity here)
 template <class F>
-BLS_HDNI jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
+BLS_INL jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
   if (jac_is_inf(p)) return jac_from_aff(q);
   F Z1Z1 = F_sqr(p.z);
   F U2 = F_mul(q.x, Z1Z1);
@@ -113,7 +113,7 @@ BLS_HDNI jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
 
 // general Jacobian addition
 template <class F>
-BLS_HDNI jac<F> jac_add(const jac<F>& p, const jac<F>& q) {
+BLS_INL jac<F> jac_add(const jac<F>& p, const jac<F>& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
   F Z1Z1 = F_sqr(p.z);

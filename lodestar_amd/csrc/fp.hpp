@@ -18,15 +18,30 @@
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
-#define BLS_HD __host__ __device__ __forceinline__
-#define BLS_HDNI __host__ __device__ __noinline__
-// Medium/large arithmetic (a Montgomery product is ~450 instructions) is emitted once as a real device
-// function: inlining everything into every kernel makes multi-hour compiles of multi-MB code objects.
-#define BLS_FN __host__ __device__ __noinline__
+// Device-only under hipcc: the host pass of a kernel TU must not compile (and fully inline) the
+// arithmetic for x86.  The host build of the same headers (tests/native/emu.cpp, g++) takes the #else.
+#define BLS_HD __device__ __forceinline__
+// Call-granularity policy.  AMDGPU passes aggregate arguments larger than 16 dwords through scratch and
+// a caller cannot keep its live values in registers a callee may clobber, so a device function whose
+// arguments are Fp/Fp2/Fp12 values costs a scratch round trip per call.  Therefore:
+//   * the two Montgomery products are register-ABI calls (fp_mul_r / fp_sqr_r below: operands as 28 / 14
+//     scalar VGPR arguments, the 14-dword result returned in VGPRs -- no scratch, ~42 v_mov per call),
+//     which keeps every call site ~50 instructions and the compile time of the whole pipeline small;
+//   * everything between a product and a coarse loop (Fp/Fp2/Fp6/Fp12 algebra, point formulas, Miller
+//     steps) is inlined, so it runs on register-resident values;
+//   * only coarse operations that loop internally (exponentiations, scalar multiplications, the Miller
+//     loop, the final exponentiation, decoders) are real device functions (BLS_BIG / BLS_HDNI), where the
+//     argument round trip is negligible next to their work.
+#define BLS_INL __device__ __forceinline__
+#define BLS_BIG __device__ __noinline__
+#define BLS_HDNI BLS_BIG
+#define BLS_FN BLS_INL
 #else
 #define BLS_HD static inline
 #define BLS_HDNI static
-#define BLS_FN static
+#define BLS_FN static inline
+#define BLS_INL static inline
+#define BLS_BIG static
 #endif
 #define BLS_CONST static constexpr
 
@@ -55,8 +70,7 @@ extern unsigned long long bls_count_mul, bls_count_sqr;
 // ------------------------------------------------------------------------------------------------
 // Montgomery multiplication: finely integrated product scanning (column-wise a*b and m*p).
 // ------------------------------------------------------------------------------------------------
-BLS_FN fp fp_mul(const fp& a, const fp& b) {
-  BLS_COUNT(bls_count_mul);
+BLS_INL fp fp_mul_body(const fp& a, const fp& b) {
   fp r;
   uint32_t m[BLS_NL];
   uint64_t acc = 0;
@@ -85,8 +99,7 @@ BLS_FN fp fp_mul(const fp& a, const fp& b) {
   return r;
 }
 
-BLS_FN fp fp_sqr(const fp& a) {
-  BLS_COUNT(bls_count_sqr);
+BLS_INL fp fp_sqr_body(const fp& a) {
   fp r;
   uint32_t m[BLS_NL];
   uint32_t a2[BLS_NL];
@@ -118,6 +131,59 @@ BLS_FN fp fp_sqr(const fp& a) {
   r.l[BLS_NL - 1] = (uint32_t)acc;
   return r;
 }
+
+// Register-ABI product boundary (see the call-granularity policy above).  BLS_INLINE_PRODUCTS=1 inlines
+// the bodies instead (bigger code, slower compiles; for experiments).
+#if defined(__HIP_DEVICE_COMPILE__) && !BLS_INLINE_PRODUCTS
+struct fp_ret {
+  uint32_t l[BLS_NL];
+};
+#define BLS_ARGS14(x) \
+  x.l[0], x.l[1], x.l[2], x.l[3], x.l[4], x.l[5], x.l[6], x.l[7], x.l[8], x.l[9], x.l[10], x.l[11], x.l[12], x.l[13]
+#define BLS_PARAMS14(x)                                                                                     \
+  uint32_t x##0, uint32_t x##1, uint32_t x##2, uint32_t x##3, uint32_t x##4, uint32_t x##5, uint32_t x##6, \
+      uint32_t x##7, uint32_t x##8, uint32_t x##9, uint32_t x##10, uint32_t x##11, uint32_t x##12, uint32_t x##13
+#define BLS_INIT14(x) {{x##0, x##1, x##2, x##3, x##4, x##5, x##6, x##7, x##8, x##9, x##10, x##11, x##12, x##13}}
+__device__ __noinline__ fp_ret fp_mul_r(BLS_PARAMS14(a), BLS_PARAMS14(b)) {
+  const fp x = BLS_INIT14(a), y = BLS_INIT14(b);
+  const fp r = fp_mul_body(x, y);
+  fp_ret o;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) o.l[i] = r.l[i];
+  return o;
+}
+__device__ __noinline__ fp_ret fp_sqr_r(BLS_PARAMS14(a)) {
+  const fp x = BLS_INIT14(a);
+  const fp r = fp_sqr_body(x);
+  fp_ret o;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) o.l[i] = r.l[i];
+  return o;
+}
+__device__ __forceinline__ fp fp_mul(const fp& a, const fp& b) {
+  const fp_ret t = fp_mul_r(BLS_ARGS14(a), BLS_ARGS14(b));
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = t.l[i];
+  return r;
+}
+__device__ __forceinline__ fp fp_sqr(const fp& a) {
+  const fp_ret t = fp_sqr_r(BLS_ARGS14(a));
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = t.l[i];
+  return r;
+}
+#else
+BLS_INL fp fp_mul(const fp& a, const fp& b) {
+  BLS_COUNT(bls_count_mul);
+  return fp_mul_body(a, b);
+}
+BLS_INL fp fp_sqr(const fp& a) {
+  BLS_COUNT(bls_count_sqr);
+  return fp_sqr_body(a);
+}
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // Additive operations (keep value <= 2p, limbs normalized)

@@ -1,0 +1,134 @@
+// Shared device helpers of the verification kernels: SoA limb-major loads/stores (element i, word w at
+// base[w * stride + i], so the 64 lanes of a wave touch 64 consecutive words per limb -- coalesced) and
+// the small scalar-multiplication loops.  Included by every k_*.hip translation unit.
+#pragma once
+#include "kernels.h"
+#include "ops.hpp"
+
+#define WAVE 64
+
+__device__ __forceinline__ fp ld_fp(const uint32_t* p, uint32_t n, uint32_t i, int w0) {
+  fp r;
+#pragma unroll
+  for (int l = 0; l < BLS_NL; l++) r.l[l] = p[(size_t)(w0 + l) * n + i];
+  return r;
+}
+__device__ __forceinline__ void st_fp(uint32_t* p, uint32_t n, uint32_t i, int w0, const fp& v) {
+#pragma unroll
+  for (int l = 0; l < BLS_NL; l++) p[(size_t)(w0 + l) * n + i] = v.l[l];
+}
+__device__ __forceinline__ fp2 ld_fp2(const uint32_t* p, uint32_t n, uint32_t i, int w0) {
+  return fp2_make(ld_fp(p, n, i, w0), ld_fp(p, n, i, w0 + W_FP));
+}
+__device__ __forceinline__ void st_fp2(uint32_t* p, uint32_t n, uint32_t i, int w0, const fp2& v) {
+  st_fp(p, n, i, w0, v.c0);
+  st_fp(p, n, i, w0 + W_FP, v.c1);
+}
+__device__ __forceinline__ g2a ld_g2a(const uint32_t* p, uint32_t n, uint32_t i) {
+  g2a r;
+  r.x = ld_fp2(p, n, i, 0);
+  r.y = ld_fp2(p, n, i, 2 * W_FP);
+  return r;
+}
+__device__ __forceinline__ void st_g2a(uint32_t* p, uint32_t n, uint32_t i, const g2a& v) {
+  st_fp2(p, n, i, 0, v.x);
+  st_fp2(p, n, i, 2 * W_FP, v.y);
+}
+__device__ __forceinline__ g2j ld_g2j(const uint32_t* p, uint32_t n, uint32_t i) {
+  g2j r;
+  r.x = ld_fp2(p, n, i, 0);
+  r.y = ld_fp2(p, n, i, 2 * W_FP);
+  r.z = ld_fp2(p, n, i, 4 * W_FP);
+  return r;
+}
+__device__ __forceinline__ void st_g2j(uint32_t* p, uint32_t n, uint32_t i, const g2j& v) {
+  st_fp2(p, n, i, 0, v.x);
+  st_fp2(p, n, i, 2 * W_FP, v.y);
+  st_fp2(p, n, i, 4 * W_FP, v.z);
+}
+__device__ __forceinline__ g1a ld_g1a(const uint32_t* p, uint32_t n, uint32_t i) {
+  g1a r;
+  r.x = ld_fp(p, n, i, 0);
+  r.y = ld_fp(p, n, i, W_FP);
+  return r;
+}
+__device__ __forceinline__ void st_g1a(uint32_t* p, uint32_t n, uint32_t i, const g1a& v) {
+  st_fp(p, n, i, 0, v.x);
+  st_fp(p, n, i, W_FP, v.y);
+}
+__device__ __forceinline__ g1j ld_g1j(const uint32_t* p, uint32_t n, uint32_t i) {
+  g1j r;
+  r.x = ld_fp(p, n, i, 0);
+  r.y = ld_fp(p, n, i, W_FP);
+  r.z = ld_fp(p, n, i, 2 * W_FP);
+  return r;
+}
+__device__ __forceinline__ void st_g1j(uint32_t* p, uint32_t n, uint32_t i, const g1j& v) {
+  st_fp(p, n, i, 0, v.x);
+  st_fp(p, n, i, W_FP, v.y);
+  st_fp(p, n, i, 2 * W_FP, v.z);
+}
+__device__ __forceinline__ fp12 ld_fp12(const uint32_t* p, uint32_t n, uint32_t i) {
+  fp12 f;
+  f.c0.c0 = ld_fp2(p, n, i, 0);
+  f.c0.c1 = ld_fp2(p, n, i, 2 * W_FP);
+  f.c0.c2 = ld_fp2(p, n, i, 4 * W_FP);
+  f.c1.c0 = ld_fp2(p, n, i, 6 * W_FP);
+  f.c1.c1 = ld_fp2(p, n, i, 8 * W_FP);
+  f.c1.c2 = ld_fp2(p, n, i, 10 * W_FP);
+  return f;
+}
+__device__ __forceinline__ void st_fp12(uint32_t* p, uint32_t n, uint32_t i, const fp12& f) {
+  st_fp2(p, n, i, 0, f.c0.c0);
+  st_fp2(p, n, i, 2 * W_FP, f.c0.c1);
+  st_fp2(p, n, i, 4 * W_FP, f.c0.c2);
+  st_fp2(p, n, i, 6 * W_FP, f.c1.c0);
+  st_fp2(p, n, i, 8 * W_FP, f.c1.c1);
+  st_fp2(p, n, i, 10 * W_FP, f.c1.c2);
+}
+__device__ __forceinline__ g1a ld_pktab(const uint32_t* tab, uint32_t idx) {
+  const uint4* q = reinterpret_cast<const uint4*>(tab + (size_t)idx * W_PKTAB);
+  uint32_t w[W_PKTAB];
+#pragma unroll
+  for (int k = 0; k < W_PKTAB / 4; k++) {
+    uint4 v = q[k];
+    w[4 * k] = v.x;
+    w[4 * k + 1] = v.y;
+    w[4 * k + 2] = v.z;
+    w[4 * k + 3] = v.w;
+  }
+  g1a r;
+#pragma unroll
+  for (int l = 0; l < BLS_NL; l++) {
+    r.x.l[l] = w[l];
+    r.y.l[l] = w[BLS_NL + l];
+  }
+  return r;
+}
+
+// [k]P for Jacobian P
+template <class F>
+__device__ jac<F> jac_mul_u64_j(const jac<F>& P, uint64_t k) {
+  jac<F> r = jac_infinity<F>();
+  if (k == 0) return r;
+  int top = 63;
+  while (((k >> top) & 1ull) == 0) top--;
+  r = P;
+  for (int i = top - 1; i >= 0; i--) {
+    r = jac_dbl(r);
+    if ((k >> i) & 1ull) r = jac_add(r, P);
+  }
+  return r;
+}
+
+// [k]P for a multi-word scalar (little-endian 32-bit words), used by the workload-generation ops
+template <class F>
+__device__ jac<F> jac_mul_words(const jac<F>& P, const uint32_t* k, int nw) {
+  jac<F> r = jac_infinity<F>();
+  for (int i = 32 * nw - 1; i >= 0; i--) {
+    r = jac_dbl(r);
+    if ((k[i >> 5] >> (i & 31)) & 1u) r = jac_add(r, P);
+  }
+  return r;
+}
+

@@ -1,0 +1,124 @@
+// Element-wise test hooks behind blsgpu_debug_op (stage parity tests and workload generation).
+#include "k_common.hpp"
+
+__device__ fp dbg_load_fp(const uint8_t* b) {
+  fp x;
+  fp_from_be48_plain(b, x, 0xff);
+  return fp_to_mont(x);
+}
+__device__ fp2 dbg_load_fp2(const uint8_t* b) { return fp2_make(dbg_load_fp(b + 48), dbg_load_fp(b)); }
+__device__ g2a dbg_load_g2(const uint8_t* b) {
+  g2a p;
+  p.x = dbg_load_fp2(b);
+  p.y = dbg_load_fp2(b + 96);
+  return p;
+}
+__device__ g1a dbg_load_g1(const uint8_t* b) {
+  g1a p;
+  p.x = dbg_load_fp(b);
+  p.y = dbg_load_fp(b + 48);
+  return p;
+}
+__device__ void dbg_store_fp12(const fp12& f, uint8_t* b) {
+  const fp2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int k = 0; k < 6; k++) {
+    fp_to_be48(c[k]->c0, b + 96 * k);
+    fp_to_be48(c[k]->c1, b + 96 * k + 48);
+  }
+}
+__device__ fp12 dbg_load_fp12(const uint8_t* b) {
+  fp12 f;
+  fp2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int k = 0; k < 6; k++) {
+    c[k]->c0 = dbg_load_fp(b + 96 * k);
+    c[k]->c1 = dbg_load_fp(b + 96 * k + 48);
+  }
+  return f;
+}
+
+__global__ __launch_bounds__(WAVE) void k_debug_op(int op, uint32_t n, const uint8_t* in, uint32_t in_stride,
+                                                   uint8_t* out, uint32_t out_stride, int32_t* status) {
+  uint32_t i = blockIdx.x * WAVE + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* a = in + (size_t)i * in_stride;
+  uint8_t* o = out + (size_t)i * out_stride;
+  int st = 0;
+  switch (op) {
+    case 0:
+      fp_to_be48(fp_mul(dbg_load_fp(a), dbg_load_fp(a + 48)), o);
+      break;
+    case 1: {
+      uint32_t len = (uint32_t)a[192] | ((uint32_t)a[193] << 8);
+      g2a p;
+      bool inf;
+      st = sig_decode(a, len, p, inf);
+      if (st == 0 && !inf) g2a_to_be192(p, o);
+      if (st == 0 && inf) st = -1;
+      break;
+    }
+    case 2: {
+      g2a p;
+      st = jac_to_aff(hash_to_g2_jac(a), p) ? 0 : -1;
+      if (st == 0) g2a_to_be192(p, o);
+      break;
+    }
+    case 3:
+      dbg_store_fp12(miller_loop(dbg_load_g1(a), dbg_load_g2(a + 96)), o);
+      break;
+    case 4:
+      dbg_store_fp12(final_exponentiation(dbg_load_fp12(a)), o);
+      break;
+    case 5: {
+      uint64_t k = 0;
+      for (int j = 0; j < 8; j++) k |= (uint64_t)a[96 + j] << (8 * j);
+      g1a r;
+      st = jac_to_aff(jac_mul_u64(dbg_load_g1(a), k), r) ? 0 : -1;
+      if (st == 0) g1a_to_be96(r, o);
+      break;
+    }
+    case 6: {
+      uint64_t k = 0;
+      for (int j = 0; j < 8; j++) k |= (uint64_t)a[192 + j] << (8 * j);
+      g2a r;
+      st = jac_to_aff(jac_mul_u64(dbg_load_g2(a), k), r) ? 0 : -1;
+      if (st == 0) g2a_to_be192(r, o);
+      break;
+    }
+    case 7: {  // sign: sk (32 B big-endian) || msg (32 B) -> compressed signature (96 B)
+      uint32_t w[8];
+      for (int j = 0; j < 8; j++)
+        w[j] = ((uint32_t)a[31 - 4 * j]) | ((uint32_t)a[30 - 4 * j] << 8) | ((uint32_t)a[29 - 4 * j] << 16) |
+               ((uint32_t)a[28 - 4 * j] << 24);
+      g2j h = hash_to_g2_jac(a + 32);
+      g2a ha;
+      st = jac_to_aff(h, ha) ? 0 : -1;
+      g2a s;
+      if (st == 0) st = jac_to_aff(jac_mul_words(jac_from_aff(ha), w, 8), s) ? 0 : -1;
+      if (st == 0) g2a_compress(s, o);
+      break;
+    }
+    case 8: {  // sk_to_pk: sk (32 B big-endian) -> uncompressed pubkey (96 B)
+      uint32_t w[8];
+      for (int j = 0; j < 8; j++)
+        w[j] = ((uint32_t)a[31 - 4 * j]) | ((uint32_t)a[30 - 4 * j] << 8) | ((uint32_t)a[29 - 4 * j] << 16) |
+               ((uint32_t)a[28 - 4 * j] << 24);
+      g1a g;
+      g.x = G1_GEN_X;
+      g.y = G1_GEN_Y;
+      g1a pk;
+      st = jac_to_aff(jac_mul_words(jac_from_aff(g), w, 8), pk) ? 0 : -1;
+      if (st == 0) g1a_to_be96(pk, o);
+      break;
+    }
+    default:
+      st = -2;
+  }
+  status[i] = st;
+}
+
+static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
+
+void launch_debug_op(int op, uint32_t n, const uint8_t* in, uint32_t in_stride, uint8_t* out, uint32_t out_stride,
+                     int32_t* status, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_debug_op, grid_for(n), dim3(WAVE), 0, s, op, n, in, in_stride, out, out_stride, status);
+}

@@ -53,22 +53,29 @@ BLS_FN void miller_add_step(g2proj& T, const g2a& Q, const fp& xP, const fp& yP,
 }
 
 // f = conj(f_{|z|,Q}(P)).  P, Q affine and not infinity.
+// The 68 steps (63 doublings, 5 additions) run as one flat loop with a single copy of each step body:
+// a doubling step squares f first (except the very first), an addition step does not.
 BLS_HDNI fp12 miller_loop(const g1a& P, const g2a& Q) {
   g2proj T;
   T.x = Q.x;
   T.y = Q.y;
   T.z = fp2_one();
   fp12 f = fp12_one();
-  fp2 l0, l1, l4;
-  // top bit (63) of |z| consumed by T = Q
-  for (int i = 62; i >= 0; i--) {
-    if (i != 62) f = fp12_sqr(f);
-    miller_dbl_step(T, P.x, P.y, l0, l1, l4);
-    f = fp12_mul_by_014(f, l0, l1, l4);
-    if ((BLS_Z_ABS >> i) & 1ull) {
+  int bit = 62;
+  bool add_next = false;
+#pragma unroll 1
+  for (int s = 0; s < 68; s++) {
+    fp2 l0, l1, l4;
+    if (!add_next) {
+      if (s != 0) f = fp12_sqr(f);
+      miller_dbl_step(T, P.x, P.y, l0, l1, l4);
+      add_next = (BLS_Z_ABS >> bit) & 1ull;
+      bit--;
+    } else {
       miller_add_step(T, Q, P.x, P.y, l0, l1, l4);
-      f = fp12_mul_by_014(f, l0, l1, l4);
+      add_next = false;
     }
+    f = fp12_mul_by_014(f, l0, l1, l4);
   }
   return fp12_conj(f);
 }
@@ -84,14 +91,17 @@ BLS_HDNI fp12 fp12_pow_zabs(const fp12& f) {
 }
 BLS_HD fp12 fp12_pow_z(const fp12& f) { return fp12_conj(fp12_pow_zabs(f)); }
 
+// Coarse (called) Fp12 product for the straight-line part of the final exponentiation.
+BLS_BIG fp12 fp12_mul_c(const fp12& a, const fp12& b) { return fp12_mul(a, b); }
+
 // Final exponentiation, returns e^3 (same "== 1" answer since gcd(3, r) = 1):
 //   easy part (p^6 - 1)(p^2 + 1), hard part 3(p^4 - p^2 + 1)/r = (z-1)^2 (z+p)(z^2+p^2-1) + 3
 BLS_HDNI fp12 final_exponentiation(const fp12& f) {
-  fp12 f1 = fp12_mul(fp12_conj(f), fp12_inv(f));
-  fp12 m = fp12_mul(fp12_frob2(f1), f1);
-  fp12 t = fp12_mul(fp12_pow_z(m), fp12_conj(m));
-  t = fp12_mul(fp12_pow_z(t), fp12_conj(t));
-  t = fp12_mul(fp12_pow_z(t), fp12_frob1(t));
-  t = fp12_mul(fp12_mul(fp12_pow_z(fp12_pow_z(t)), fp12_frob2(t)), fp12_conj(t));
-  return fp12_mul(t, fp12_mul(fp12_sqr(m), m));
+  fp12 f1 = fp12_mul_c(fp12_conj(f), fp12_inv(f));
+  fp12 m = fp12_mul_c(fp12_frob2(f1), f1);
+  fp12 t = fp12_mul_c(fp12_pow_z(m), fp12_conj(m));
+  t = fp12_mul_c(fp12_pow_z(t), fp12_conj(t));
+  t = fp12_mul_c(fp12_pow_z(t), fp12_frob1(t));
+  t = fp12_mul_c(fp12_mul_c(fp12_pow_z(fp12_pow_z(t)), fp12_frob2(t)), fp12_conj(t));
+  return fp12_mul_c(t, fp12_mul_c(fp12_sqr(m), m));
 }

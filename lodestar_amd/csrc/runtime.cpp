@@ -2,15 +2,21 @@
 //
 // Replaces BlsMultiThreadWorkerPool's job plumbing (reference packages/beacon-node/src/chain/bls/
 // multithread/index.ts:134-412) and the worker's batch/fallback policy (multithread/worker.ts:32-108)
-// with one HIP stream per MI355X and no worker threads:
+// with HIP streams on MI355X and no worker threads doing arithmetic:
 //   * jobs are sharded across devices in contiguous, cost-balanced ranges (never splitting a job);
-//   * each device verifies its shard with the kernel pipeline of kernels.hip;
-//   * batchable jobs are grouped (random linear combination, one final exponentiation per group);
-//     non-batchable jobs are their own group, single-set non-batchable jobs use r = 1 (= CoreVerify,
-//     maybeBatch.ts:34-38);
-//   * a failed group with several jobs is re-checked per job (worker.ts:76-98), reusing the per-set
-//     Miller loops already on the device: only the per-job sum(r sig), one Miller loop and one final
-//     exponentiation per job are recomputed.
+//   * each device owns several "slots" (a HIP stream + its staging and work buffers).  A call takes one
+//     free slot per device it uses, so independent verifySignatureSets calls run concurrently on the
+//     GPU -- the way the reference keeps all its workers busy -- and the device is filled by several
+//     batches' lane-per-set kernels at once;
+//   * each shard runs the stage kernels (k_*.hip): signature decode + subgroup check, hash_to_G2,
+//     pubkey aggregation, r_i scaling, per-set Miller loops, then the batch-group tail;
+//   * batchable jobs are packed into groups of >= group_sets sets (random linear combination, one final
+//     exponentiation per group); non-batchable jobs are their own group; a single-set non-batchable
+//     job uses r = 1 (= CoreVerify, maybeBatch.ts:34-38);
+//   * a failed group with several clean jobs is split into <= 8 contiguous sub-ranges that are re-checked
+//     with the same group kernels (k-ary bisection) until every job is resolved on its own.  The per-set
+//     Miller loops stay on the device, so a re-check costs one Miller loop + final exponentiation.
+//     Per job the answer is the reference's: valid iff every set of the job verifies (worker.ts:76-98).
 // There is no CPU verification path: without a usable GPU blsgpu_init fails.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,6 +28,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -34,9 +41,9 @@ namespace {
 struct HipError {
   hipError_t e;
 };
-#define HIPCHK(x)                           \
-  do {                                      \
-    hipError_t _e = (x);                    \
+#define HIPCHK(x)                             \
+  do {                                        \
+    hipError_t _e = (x);                      \
     if (_e != hipSuccess) throw HipError{_e}; \
   } while (0)
 
@@ -78,30 +85,81 @@ struct HostBuf {  // pinned staging
   }
 };
 
-struct Device {
-  int id = 0;
+constexpr int kStages = 8;
+
+// One in-flight batch on one device: a stream and every per-call buffer.
+struct Slot {
   hipStream_t stream = nullptr;
-  std::mutex mu;
-  // pubkey table (AoS, W_PKTAB words per key)
-  DevBuf<uint32_t> table;
-  uint32_t table_n = 0;
-  // per-call buffers
-  DevBuf<uint8_t> d_sigs, d_msgs, d_pkb, d_flags, d_ok;
-  DevBuf<int8_t> d_status;
-  DevBuf<uint32_t> d_siglen, d_pkfirst, d_pkidx, d_groups, d_work, d_fgroup;
+  hipEvent_t ev[kStages + 1] = {};
+  DevBuf<uint8_t> d_sigs, d_msgs, d_pkb, d_flags, d_ok, d_include;
+  DevBuf<int8_t> d_status, d_joberr;
+  DevBuf<uint32_t> d_siglen, d_pkfirst, d_pkidx, d_jobs, d_ranges, d_work, d_S, d_F;
   DevBuf<uint64_t> d_scalars;
   HostBuf<uint8_t> h_sigs, h_msgs, h_pkb, h_ok;
-  HostBuf<int8_t> h_status;
-  HostBuf<uint32_t> h_siglen, h_pkfirst, h_pkidx, h_groups;
+  HostBuf<int8_t> h_joberr;
+  HostBuf<uint32_t> h_siglen, h_pkfirst, h_pkidx, h_jobs, h_ranges;
   HostBuf<uint64_t> h_scalars;
 
   void release_all() {
-    table.release();
     d_sigs.release(); d_msgs.release(); d_pkb.release(); d_flags.release(); d_ok.release();
-    d_status.release(); d_siglen.release(); d_pkfirst.release(); d_pkidx.release(); d_groups.release();
-    d_work.release(); d_fgroup.release(); d_scalars.release();
-    h_sigs.release(); h_msgs.release(); h_pkb.release(); h_ok.release(); h_status.release();
-    h_siglen.release(); h_pkfirst.release(); h_pkidx.release(); h_groups.release(); h_scalars.release();
+    d_include.release(); d_status.release(); d_joberr.release(); d_siglen.release(); d_pkfirst.release();
+    d_pkidx.release(); d_jobs.release(); d_ranges.release(); d_work.release(); d_S.release(); d_F.release();
+    d_scalars.release();
+    h_sigs.release(); h_msgs.release(); h_pkb.release(); h_ok.release(); h_joberr.release();
+    h_siglen.release(); h_pkfirst.release(); h_pkidx.release(); h_jobs.release(); h_ranges.release();
+    h_scalars.release();
+  }
+};
+
+struct Device {
+  int id = 0;
+  hipStream_t table_stream = nullptr;
+  // pubkey table (AoS, W_PKTAB words per key): verification holds it shared, uploads exclusive
+  std::shared_mutex table_mu;
+  DevBuf<uint32_t> table;
+  uint32_t table_n = 0;
+  // slots
+  std::mutex slot_mu;
+  std::condition_variable slot_cv;
+  std::vector<Slot*> slots;
+  std::vector<Slot*> free_slots;
+
+  void add_slot() {
+    Slot* s = new Slot();
+    HIPCHK(hipSetDevice(id));
+    HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
+    slots.push_back(s);
+    free_slots.push_back(s);
+  }
+  Slot* acquire() {
+    std::unique_lock<std::mutex> lk(slot_mu);
+    slot_cv.wait(lk, [&] { return !free_slots.empty(); });
+    Slot* s = free_slots.back();
+    free_slots.pop_back();
+    return s;
+  }
+  void release(Slot* s) {
+    {
+      std::lock_guard<std::mutex> lk(slot_mu);
+      free_slots.push_back(s);
+    }
+    slot_cv.notify_one();
+  }
+  void destroy_all() {
+    (void)hipSetDevice(id);
+    for (Slot* s : slots) {
+      if (s->stream) (void)hipStreamSynchronize(s->stream);
+      s->release_all();
+      for (auto& e : s->ev)
+        if (e) (void)hipEventDestroy(e);
+      if (s->stream) (void)hipStreamDestroy(s->stream);
+      delete s;
+    }
+    slots.clear();
+    free_slots.clear();
+    table.release();
+    if (table_stream) (void)hipStreamDestroy(table_stream);
   }
 };
 
@@ -123,8 +181,10 @@ struct blsgpu_ctx {
   std::mutex async_mu;
   std::condition_variable async_cv;
   std::mutex table_mu;
-  int64_t group_sets = 64;
+  std::mutex opt_mu;
+  int64_t group_sets = 256;
   int64_t max_devices = 64;
+  int64_t split_ways = 8;
   bool profile = false;
 };
 
@@ -135,10 +195,9 @@ struct Shard {
   uint32_t set_begin, set_end;  // set range
 };
 
-// Runs one device's shard.  Writes job_result[job_begin..job_end).
-int run_shard(blsgpu_ctx* ctx, Device& d, const blsgpu_batch& b, const Shard& sh, int8_t* job_result,
+// Runs one device's shard on one slot.  Writes job_result[job_begin..job_end).
+int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_t* job_result,
               uint64_t seed, blsgpu_stats& st) {
-  std::lock_guard<std::mutex> lk(d.mu);
   const uint32_t n = sh.set_end - sh.set_begin;
   const uint32_t nj = sh.job_end - sh.job_begin;
   if (nj == 0) return BLSGPU_OK;
@@ -146,141 +205,148 @@ int run_shard(blsgpu_ctx* ctx, Device& d, const blsgpu_batch& b, const Shard& sh
   const bool table_mode = b.pk_bytes == nullptr;
   const uint32_t s0 = sh.set_begin;
   const uint32_t stride = std::max<uint32_t>(n, 1);
+  const uint32_t split_ways = (uint32_t)std::max<int64_t>(2, ctx->split_ways);
 
-  // ---- host-side job structure: groups, scalars ---------------------------------------------
-  // A group is a contiguous run of jobs checked with one final exponentiation.  Non-batchable jobs
-  // are groups of their own; consecutive batchable jobs are packed until a group holds
-  // >= group_sets sets.  Empty jobs get no group (rejected below).
+  // ---- host-side job structure: groups (contiguous job ranges), scalars ------------------------
+  // Non-batchable jobs are groups of their own; consecutive batchable jobs are packed until a group
+  // holds >= group_sets sets.  Empty jobs get no group (rejected with EMPTY_SET).
   std::vector<uint32_t> job_group(nj, UINT32_MAX);
-  std::vector<uint32_t> group_jobs;  // jobs per group
-  d.h_scalars.ensure(stride);
-  uint64_t* scal = d.h_scalars.p;
+  std::vector<std::pair<uint32_t, uint32_t>> group_jobs;  // [first job, end job) (shard-relative)
+  sl.h_scalars.ensure(stride);
+  uint64_t* scal = sl.h_scalars.p;
+  sl.h_jobs.ensure(nj + 1);
   {
-    uint32_t cur = UINT32_MAX, cur_sets = 0;
+    uint32_t cur_sets = 0;
+    bool open = false;
     for (uint32_t j = 0; j < nj; j++) {
       const uint32_t gj = sh.job_begin + j;
       const uint32_t a = b.job_first_set[gj] - s0, e = b.job_first_set[gj + 1] - s0;
+      sl.h_jobs.p[j] = a;
       const bool batchable = b.job_flags && (b.job_flags[gj] & 1u);
-      if (e == a) continue;
+      if (e == a) {
+        open = false;
+        continue;
+      }
       if (!batchable) {
         job_group[j] = (uint32_t)group_jobs.size();
-        group_jobs.push_back(1);
+        group_jobs.push_back({j, j + 1});
         // single-set non-batchable job: CoreVerify (r = 1); multi-set: random linear combination
         for (uint32_t i = a; i < e; i++) scal[i] = (e - a == 1) ? 1ull : splitmix64_at(seed, s0 + i);
-        cur = UINT32_MAX;
+        open = false;
         continue;
       }
       for (uint32_t i = a; i < e; i++) scal[i] = splitmix64_at(seed, s0 + i);
-      if (cur == UINT32_MAX || cur_sets >= (uint32_t)ctx->group_sets) {
-        cur = (uint32_t)group_jobs.size();
-        group_jobs.push_back(0);
+      if (!open || cur_sets >= (uint32_t)ctx->group_sets) {
+        group_jobs.push_back({j, j});
         cur_sets = 0;
+        open = true;
       }
-      job_group[j] = cur;
-      group_jobs[cur]++;
+      job_group[j] = (uint32_t)group_jobs.size() - 1;
+      group_jobs.back().second = j + 1;
       cur_sets += e - a;
     }
+    sl.h_jobs.p[nj] = n;
   }
-  const uint32_t ng = (uint32_t)group_jobs.size();
-  // group g = [first set of its first job, end of its last job): contiguous by construction
-  std::vector<uint32_t> gfirst(ng, UINT32_MAX), gend(ng, 0);
-  for (uint32_t j = 0; j < nj; j++) {
-    const uint32_t g = job_group[j];
-    if (g == UINT32_MAX) continue;
+  auto job_sets = [&](uint32_t j) {
     const uint32_t gj = sh.job_begin + j;
-    gfirst[g] = std::min(gfirst[g], b.job_first_set[gj] - s0);
-    gend[g] = std::max(gend[g], b.job_first_set[gj + 1] - s0);
-  }
-  // kernels take groups as [group_first[g], group_first[g+1]); groups may be separated by the sets
-  // of nothing (empty jobs have no sets), so consecutive groups are adjacent.
-  std::vector<uint32_t> group_first(ng + 1, 0);
-  for (uint32_t g = 0; g < ng; g++) group_first[g] = gfirst[g];
-  group_first[ng] = ng ? gend[ng - 1] : 0;
+    return std::make_pair(b.job_first_set[gj] - s0, b.job_first_set[gj + 1] - s0);
+  };
 
   // ---- stage inputs (pinned) and copy to the device --------------------------------------------
   const uint32_t sstride = b.sig_stride;
-  d.h_sigs.ensure((size_t)stride * 192);
-  d.h_siglen.ensure(stride);
-  d.h_msgs.ensure((size_t)stride * 32);
+  sl.h_sigs.ensure((size_t)stride * 192);
+  sl.h_siglen.ensure(stride);
+  sl.h_msgs.ensure((size_t)stride * 32);
   for (uint32_t i = 0; i < n; i++) {
     uint32_t len = b.sig_len[s0 + i];
     uint32_t cl = (len == 96 || len == 192) ? len : 0;
-    memcpy(d.h_sigs.p + (size_t)i * 192, b.sigs + (size_t)(s0 + i) * sstride, cl);
-    d.h_siglen.p[i] = len;
+    memcpy(sl.h_sigs.p + (size_t)i * 192, b.sigs + (size_t)(s0 + i) * sstride, cl);
+    sl.h_siglen.p[i] = len;
   }
-  memcpy(d.h_msgs.p, b.msgs + (size_t)s0 * 32, (size_t)n * 32);
+  memcpy(sl.h_msgs.p, b.msgs + (size_t)s0 * 32, (size_t)n * 32);
   uint32_t npk = 0;
   if (table_mode) {
-    d.h_pkfirst.ensure(stride + 1);
+    sl.h_pkfirst.ensure(stride + 1);
     uint32_t base = b.set_pk_first[s0];
     npk = b.set_pk_first[sh.set_end] - base;
-    for (uint32_t i = 0; i <= n; i++) d.h_pkfirst.p[i] = b.set_pk_first[s0 + i] - base;
-    d.h_pkidx.ensure(std::max<uint32_t>(npk, 1));
-    memcpy(d.h_pkidx.p, b.pk_index + base, (size_t)npk * 4);
+    for (uint32_t i = 0; i <= n; i++) sl.h_pkfirst.p[i] = b.set_pk_first[s0 + i] - base;
+    sl.h_pkidx.ensure(std::max<uint32_t>(npk, 1));
+    memcpy(sl.h_pkidx.p, b.pk_index + base, (size_t)npk * 4);
   } else {
-    d.h_pkb.ensure((size_t)stride * 96);
-    memcpy(d.h_pkb.p, b.pk_bytes + (size_t)s0 * 96, (size_t)n * 96);
+    sl.h_pkb.ensure((size_t)stride * 96);
+    memcpy(sl.h_pkb.p, b.pk_bytes + (size_t)s0 * 96, (size_t)n * 96);
   }
-  d.h_groups.ensure(ng + 1 + nj + 1);
-  memcpy(d.h_groups.p, group_first.data(), (ng + 1) * 4);
+  const uint32_t ng0 = (uint32_t)group_jobs.size();
+  const uint32_t max_ranges = std::max<uint32_t>(std::max(ng0, nj), 1);
+  sl.h_ranges.ensure(2 * max_ranges);
+  for (uint32_t g = 0; g < ng0; g++) {
+    sl.h_ranges.p[2 * g] = job_sets(group_jobs[g].first).first;
+    sl.h_ranges.p[2 * g + 1] = job_sets(group_jobs[g].second - 1).second;
+  }
 
-  d.d_sigs.ensure((size_t)stride * 192);
-  d.d_siglen.ensure(stride);
-  d.d_msgs.ensure((size_t)stride * 32);
-  d.d_scalars.ensure(stride);
-  d.d_flags.ensure((size_t)stride * 2);
-  d.d_status.ensure((size_t)stride * 2);
-  d.d_groups.ensure(ng + 1 + nj + 1);
-  d.d_ok.ensure(std::max<uint32_t>(ng, nj) + 1);
-  d.d_fgroup.ensure((size_t)W_FP12 * std::max<uint32_t>(std::max(ng, nj), 1));
+  sl.d_sigs.ensure((size_t)stride * 192);
+  sl.d_siglen.ensure(stride);
+  sl.d_msgs.ensure((size_t)stride * 32);
+  sl.d_scalars.ensure(stride);
+  sl.d_flags.ensure((size_t)stride * 2);
+  sl.d_status.ensure((size_t)stride * 2);
+  sl.d_include.ensure(stride);
+  sl.d_jobs.ensure(nj + 1);
+  sl.d_joberr.ensure(nj);
+  sl.d_ranges.ensure(2 * max_ranges);
+  sl.d_ok.ensure(max_ranges);
+  sl.d_S.ensure((size_t)W_G2J * max_ranges);
+  sl.d_F.ensure((size_t)W_FP12 * max_ranges);
   // work area: sig_aff, h_aff, pk_jac, pk_aff, rsig, f
   const size_t work_words = (size_t)stride * (W_G2A + W_G2A + W_G1J + W_G1A + W_G2J + W_FP12);
-  d.d_work.ensure(work_words);
-  hipStream_t s = d.stream;
-  HIPCHK(hipMemcpyAsync(d.d_sigs.p, d.h_sigs.p, (size_t)n * 192, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(d.d_siglen.p, d.h_siglen.p, (size_t)n * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(d.d_msgs.p, d.h_msgs.p, (size_t)n * 32, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(d.d_scalars.p, d.h_scalars.p, (size_t)n * 8, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(d.d_groups.p, d.h_groups.p, (size_t)(ng + 1) * 4, hipMemcpyHostToDevice, s));
+  sl.d_work.ensure(work_words);
+  hipStream_t s = sl.stream;
+  HIPCHK(hipMemcpyAsync(sl.d_sigs.p, sl.h_sigs.p, (size_t)n * 192, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(sl.d_siglen.p, sl.h_siglen.p, (size_t)n * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(sl.d_msgs.p, sl.h_msgs.p, (size_t)n * 32, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(sl.d_scalars.p, sl.h_scalars.p, (size_t)n * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(sl.d_jobs.p, sl.h_jobs.p, (size_t)(nj + 1) * 4, hipMemcpyHostToDevice, s));
+  if (ng0) HIPCHK(hipMemcpyAsync(sl.d_ranges.p, sl.h_ranges.p, (size_t)ng0 * 8, hipMemcpyHostToDevice, s));
   if (table_mode) {
-    d.d_pkfirst.ensure(stride + 1);
-    d.d_pkidx.ensure(std::max<uint32_t>(npk, 1));
-    HIPCHK(hipMemcpyAsync(d.d_pkfirst.p, d.h_pkfirst.p, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, s));
-    if (npk) HIPCHK(hipMemcpyAsync(d.d_pkidx.p, d.h_pkidx.p, (size_t)npk * 4, hipMemcpyHostToDevice, s));
+    sl.d_pkfirst.ensure(stride + 1);
+    sl.d_pkidx.ensure(std::max<uint32_t>(npk, 1));
+    HIPCHK(hipMemcpyAsync(sl.d_pkfirst.p, sl.h_pkfirst.p, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, s));
+    if (npk) HIPCHK(hipMemcpyAsync(sl.d_pkidx.p, sl.h_pkidx.p, (size_t)npk * 4, hipMemcpyHostToDevice, s));
   } else {
-    d.d_pkb.ensure((size_t)stride * 96);
-    HIPCHK(hipMemcpyAsync(d.d_pkb.p, d.h_pkb.p, (size_t)n * 96, hipMemcpyHostToDevice, s));
+    sl.d_pkb.ensure((size_t)stride * 96);
+    HIPCHK(hipMemcpyAsync(sl.d_pkb.p, sl.h_pkb.p, (size_t)n * 96, hipMemcpyHostToDevice, s));
   }
 
   PipelineBuffers pb;
   pb.n = stride;
-  pb.sigs = d.d_sigs.p;
-  pb.sig_len = d.d_siglen.p;
+  pb.sigs = sl.d_sigs.p;
+  pb.sig_len = sl.d_siglen.p;
   pb.sig_stride = 192;
-  pb.msgs = d.d_msgs.p;
-  pb.pk_bytes = table_mode ? nullptr : d.d_pkb.p;
-  pb.set_pk_first = table_mode ? d.d_pkfirst.p : nullptr;
-  pb.pk_index = table_mode ? d.d_pkidx.p : nullptr;
+  pb.msgs = sl.d_msgs.p;
+  pb.pk_bytes = table_mode ? nullptr : sl.d_pkb.p;
+  pb.set_pk_first = table_mode ? sl.d_pkfirst.p : nullptr;
+  pb.pk_index = table_mode ? sl.d_pkidx.p : nullptr;
   pb.pk_table = d.table.p;
   pb.pk_table_n = d.table_n;
-  pb.scalars = d.d_scalars.p;
-  uint32_t* w = d.d_work.p;
+  pb.scalars = sl.d_scalars.p;
+  pb.job_first_set = sl.d_jobs.p;
+  pb.n_jobs = nj;
+  uint32_t* w = sl.d_work.p;
   pb.sig_aff = w; w += (size_t)stride * W_G2A;
   pb.h_aff = w; w += (size_t)stride * W_G2A;
   pb.pk_jac = w; w += (size_t)stride * W_G1J;
   pb.pk_aff = w; w += (size_t)stride * W_G1A;
   pb.rsig = w; w += (size_t)stride * W_G2J;
   pb.f = w;
-  pb.flags = d.d_flags.p;
-  pb.status = d.d_status.p;
+  pb.flags = sl.d_flags.p;
+  pb.status = sl.d_status.p;
+  pb.job_err = sl.d_joberr.p;
+  pb.include = sl.d_include.p;
 
   // ---- kernel pipeline ---------------------------------------------------------------------------
   const bool prof = ctx->profile;
-  hipEvent_t ev[9];
-  if (prof)
-    for (int k = 0; k < 9; k++) HIPCHK(hipEventCreate(&ev[k]));
   auto mark = [&](int k) {
-    if (prof) HIPCHK(hipEventRecord(ev[k], s));
+    if (prof) HIPCHK(hipEventRecord(sl.ev[k], s));
   };
   mark(0);
   launch_sig_decode(pb, n, s);
@@ -294,103 +360,92 @@ int run_shard(blsgpu_ctx* ctx, Device& d, const blsgpu_batch& b, const Shard& sh
   launch_sig_scale(pb, n, s);
   mark(5);
   launch_miller_sets(pb, n, s);
+  launch_job_mask(pb, s);
   mark(6);
-  launch_group_sig_miller(pb, d.d_groups.p, ng, d.d_fgroup.p, s);
+  launch_group_reduce(pb, sl.d_ranges.p, ng0, sl.d_S.p, sl.d_F.p, s);
   mark(7);
-  launch_group_finish(pb, d.d_groups.p, ng, d.d_fgroup.p, d.d_ok.p, s);
+  launch_group_check(sl.d_S.p, sl.d_F.p, ng0, sl.d_ok.p, s);
   mark(8);
   HIPCHK(hipGetLastError());
-  d.h_status.ensure((size_t)stride * 2);
-  d.h_ok.ensure(std::max<uint32_t>(ng, nj) + 1);
-  HIPCHK(hipMemcpyAsync(d.h_status.p, d.d_status.p, (size_t)stride * 2, hipMemcpyDeviceToHost, s));
-  if (ng) HIPCHK(hipMemcpyAsync(d.h_ok.p, d.d_ok.p, ng, hipMemcpyDeviceToHost, s));
+  sl.h_joberr.ensure(nj);
+  sl.h_ok.ensure(max_ranges);
+  HIPCHK(hipMemcpyAsync(sl.h_joberr.p, sl.d_joberr.p, nj, hipMemcpyDeviceToHost, s));
+  if (ng0) HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, ng0, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  st.groups += ng;
+  st.groups += ng0;
   if (prof) {
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < kStages; k++) {
       float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      HIPCHK(hipEventElapsedTime(&ms, sl.ev[k], sl.ev[k + 1]));
       st.stage_ms[k] += ms;
     }
-    for (int k = 0; k < 9; k++) (void)hipEventDestroy(ev[k]);
   }
 
   // ---- per-job results ---------------------------------------------------------------------------
-  const int8_t* sig_st = d.h_status.p;
-  const int8_t* pk_st = d.h_status.p + stride;
-  std::vector<uint32_t> clean_jobs_in_group(ng, 0);
   std::vector<int> jr(nj, 0);
   for (uint32_t j = 0; j < nj; j++) {
-    uint32_t gj = sh.job_begin + j;
-    uint32_t a = b.job_first_set[gj] - s0, e = b.job_first_set[gj + 1] - s0;
-    if (a == e) {
-      jr[j] = -BLSGPU_EMPTY_SET;
-      continue;
-    }
-    int err = 0;
-    for (uint32_t i = a; i < e && !err; i++)
-      if (pk_st[i]) err = pk_st[i];
-    for (uint32_t i = a; i < e && !err; i++)
-      if (sig_st[i]) err = sig_st[i];
-    if (err) {
-      jr[j] = -err;
-      continue;
-    }
-    jr[j] = 2;  // pending
-    clean_jobs_in_group[job_group[j]]++;
+    const int err = sl.h_joberr.p[j];
+    jr[j] = err ? -err : 2;  // 2 = pending
   }
-  std::vector<uint32_t> retry;  // jobs to re-check individually
-  for (uint32_t j = 0; j < nj; j++) {
-    if (jr[j] != 2) continue;
-    uint32_t g = job_group[j];
-    if (d.h_ok.p[g]) {
-      jr[j] = 1;
-    } else if (clean_jobs_in_group[g] == 1) {
-      jr[j] = 0;
+  // pending work: lists of clean jobs whose batch equation failed
+  std::vector<std::vector<uint32_t>> failed;
+  for (uint32_t g = 0; g < ng0; g++) {
+    std::vector<uint32_t> clean;
+    for (uint32_t j = group_jobs[g].first; j < group_jobs[g].second; j++)
+      if (jr[j] == 2) clean.push_back(j);
+    if (clean.empty()) continue;
+    if (sl.h_ok.p[g]) {
+      for (uint32_t j : clean) jr[j] = 1;
+      if (group_jobs[g].second - group_jobs[g].first > 1)
+        for (uint32_t j : clean) st.batch_sigs_success += job_sets(j).second - job_sets(j).first;
+    } else if (clean.size() == 1) {
+      jr[clean[0]] = 0;
     } else {
-      retry.push_back(j);
-    }
-  }
-  for (uint32_t g = 0; g < ng; g++) {
-    if (d.h_ok.p[g]) {
-      st.batch_sigs_success += 0;  // counted per job below
-    } else if (clean_jobs_in_group[g] > 1) {
       st.batch_retries++;
+      failed.push_back(std::move(clean));
     }
-  }
-  for (uint32_t j = 0; j < nj; j++) {
-    uint32_t gj = sh.job_begin + j;
-    if (jr[j] == 1 && group_jobs[job_group[j]] > 1)
-      st.batch_sigs_success += b.job_first_set[gj + 1] - b.job_first_set[gj];
   }
 
-  // ---- fallback: each retried job becomes its own group -------------------------------------------
-  if (!retry.empty()) {
-    const uint32_t nr = (uint32_t)retry.size();
-    // groups must be contiguous set ranges: one group per retried job
-    std::vector<uint32_t> rg(nr + 1);
-    // a group is [first, last) of the job; groups are not adjacent, so pass first/last pairs by
-    // launching one group array of 2*nr entries and using even/odd views is not supported by the
-    // kernels -> issue one launch over a contiguous "group_first" built per retried job run.
-    // Retried jobs are processed in runs of adjacent jobs (contiguous sets).
-    size_t k = 0;
-    while (k < nr) {
-      size_t k2 = k + 1;
-      while (k2 < nr && retry[k2] == retry[k2 - 1] + 1) k2++;
-      const uint32_t cnt = (uint32_t)(k2 - k);
-      for (uint32_t t = 0; t <= cnt; t++) {
-        uint32_t gj = sh.job_begin + retry[k] + t;
-        rg[t] = b.job_first_set[gj] - s0;
+  // ---- fallback: k-ary bisection of failed groups -------------------------------------------------
+  while (!failed.empty()) {
+    std::vector<std::vector<uint32_t>> parts;
+    for (auto& jobs : failed) {
+      const size_t k = std::min<size_t>(split_ways, jobs.size());
+      for (size_t p = 0; p < k; p++) {
+        size_t lo = jobs.size() * p / k, hi = jobs.size() * (p + 1) / k;
+        if (hi > lo) parts.emplace_back(jobs.begin() + lo, jobs.begin() + hi);
       }
-      HIPCHK(hipMemcpyAsync(d.d_groups.p, rg.data(), (size_t)(cnt + 1) * 4, hipMemcpyHostToDevice, s));
-      launch_group_sig_miller(pb, d.d_groups.p, cnt, d.d_fgroup.p, s);
-      launch_group_finish(pb, d.d_groups.p, cnt, d.d_fgroup.p, d.d_ok.p, s);
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(d.h_ok.p, d.d_ok.p, cnt, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-      for (uint32_t t = 0; t < cnt; t++) jr[retry[k + t]] = d.h_ok.p[t] ? 1 : 0;
-      k = k2;
     }
+    const uint32_t np = (uint32_t)parts.size();
+    sl.h_ranges.ensure(2 * np);
+    sl.d_ranges.ensure(2 * np);
+    sl.d_ok.ensure(np);
+    sl.h_ok.ensure(np);
+    sl.d_S.ensure((size_t)W_G2J * np);
+    sl.d_F.ensure((size_t)W_FP12 * np);
+    for (uint32_t q = 0; q < np; q++) {
+      sl.h_ranges.p[2 * q] = job_sets(parts[q].front()).first;
+      sl.h_ranges.p[2 * q + 1] = job_sets(parts[q].back()).second;
+    }
+    // Sub-ranges may span error jobs between clean ones; their sets are masked out on the device.  A
+    // single-job part covers exactly its own sets, so every final `false` is decided on the job alone.
+    HIPCHK(hipMemcpyAsync(sl.d_ranges.p, sl.h_ranges.p, (size_t)np * 8, hipMemcpyHostToDevice, s));
+    launch_group_reduce(pb, sl.d_ranges.p, np, sl.d_S.p, sl.d_F.p, s);
+    launch_group_check(sl.d_S.p, sl.d_F.p, np, sl.d_ok.p, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, np, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<std::vector<uint32_t>> next;
+    for (uint32_t q = 0; q < np; q++) {
+      if (sl.h_ok.p[q]) {
+        for (uint32_t j : parts[q]) jr[j] = 1;
+      } else if (parts[q].size() == 1) {
+        jr[parts[q][0]] = 0;
+      } else {
+        next.push_back(std::move(parts[q]));
+      }
+    }
+    failed.swap(next);
   }
   for (uint32_t j = 0; j < nj; j++) job_result[sh.job_begin + j] = (int8_t)jr[j];
   return BLSGPU_OK;
@@ -444,7 +499,8 @@ int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
       d->id = id;
       ctx->devs.push_back(d);
       HIPCHK(hipSetDevice(id));
-      HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+      HIPCHK(hipStreamCreateWithFlags(&d->table_stream, hipStreamNonBlocking));
+      for (int k = 0; k < 4; k++) d->add_slot();
     }
   } catch (HipError&) {
     blsgpu_destroy(ctx);
@@ -462,11 +518,12 @@ void blsgpu_destroy(blsgpu_ctx* ctx) {
     ctx->async_cv.wait(lk, [&] { return ctx->inflight.load() == 0; });
   }
   for (Device* d : ctx->devs) {
-    std::lock_guard<std::mutex> lk(d->mu);
-    (void)hipSetDevice(d->id);
-    if (d->stream) (void)hipStreamSynchronize(d->stream);
-    d->release_all();
-    if (d->stream) (void)hipStreamDestroy(d->stream);
+    // wait until no synchronous caller holds a slot
+    {
+      std::unique_lock<std::mutex> lk(d->slot_mu);
+      d->slot_cv.wait(lk, [&] { return d->free_slots.size() == d->slots.size(); });
+    }
+    d->destroy_all();
     delete d;
   }
   delete ctx;
@@ -487,31 +544,33 @@ int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* 
   int result = BLSGPU_OK;
   try {
     for (Device* d : ctx->devs) {
-      std::lock_guard<std::mutex> lk(d->mu);
+      std::unique_lock<std::shared_mutex> lk(d->table_mu);
       HIPCHK(hipSetDevice(d->id));
+      hipStream_t ts = d->table_stream;
       const uint32_t need = first_index + n;
-      if (need > d->table.cap / W_PKTAB) {
-        DevBuf<uint32_t> nt;
-        nt.ensure((size_t)std::max<uint32_t>(need, d->table_n + d->table_n / 2) * W_PKTAB);
-        if (d->table_n) HIPCHK(hipMemcpy(nt.p, d->table.p, (size_t)d->table_n * W_PKTAB * 4, hipMemcpyDeviceToDevice));
-        d->table.release();
-        d->table = nt;
-      }
       uint8_t* dpk = nullptr;
       int8_t* dst = nullptr;
       uint32_t* tmp = nullptr;
       HIPCHK(hipMalloc((void**)&dpk, (size_t)n * 96));
       HIPCHK(hipMalloc((void**)&dst, n));
       HIPCHK(hipMalloc((void**)&tmp, (size_t)n * W_PKTAB * 4));
-      HIPCHK(hipMemcpyAsync(dpk, pk96, (size_t)n * 96, hipMemcpyHostToDevice, d->stream));
-      launch_pk_table_fill(dpk, n, tmp, dst, d->stream);
+      HIPCHK(hipMemcpyAsync(dpk, pk96, (size_t)n * 96, hipMemcpyHostToDevice, ts));
+      launch_pk_table_fill(dpk, n, tmp, dst, ts);
       HIPCHK(hipGetLastError());
       std::vector<int8_t> hst(n);
-      HIPCHK(hipMemcpyAsync(hst.data(), dst, n, hipMemcpyDeviceToHost, d->stream));
-      HIPCHK(hipStreamSynchronize(d->stream));
+      HIPCHK(hipMemcpyAsync(hst.data(), dst, n, hipMemcpyDeviceToHost, ts));
+      HIPCHK(hipStreamSynchronize(ts));
       int err = 0;
       for (uint32_t i = 0; i < n && !err; i++) err = hst[i];
       if (!err) {
+        if (need > d->table.cap / W_PKTAB) {
+          DevBuf<uint32_t> nt;
+          nt.ensure((size_t)std::max<uint32_t>(need, d->table_n + d->table_n / 2) * W_PKTAB);
+          if (d->table_n)
+            HIPCHK(hipMemcpy(nt.p, d->table.p, (size_t)d->table_n * W_PKTAB * 4, hipMemcpyDeviceToDevice));
+          d->table.release();
+          d->table = nt;
+        }
         HIPCHK(hipMemcpy(d->table.p + (size_t)first_index * W_PKTAB, tmp, (size_t)n * W_PKTAB * 4,
                          hipMemcpyDeviceToDevice));
         d->table_n = std::max(d->table_n, need);
@@ -533,6 +592,7 @@ int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* 
 int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return BLSGPU_ERR_ARGS;
   std::string k(key);
+  std::lock_guard<std::mutex> lk(ctx->opt_mu);
   if (k == "group_sets") {
     if (value < 1) return BLSGPU_ERR_ARGS;
     ctx->group_sets = value;
@@ -541,6 +601,19 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "max_devices") {
     if (value < 1) return BLSGPU_ERR_ARGS;
     ctx->max_devices = value;
+  } else if (k == "split_ways") {
+    if (value < 2) return BLSGPU_ERR_ARGS;
+    ctx->split_ways = value;
+  } else if (k == "slots") {
+    if (value < 1 || value > 64) return BLSGPU_ERR_ARGS;
+    try {
+      for (Device* d : ctx->devs) {
+        std::lock_guard<std::mutex> sl(d->slot_mu);
+        while ((int64_t)d->slots.size() < value) d->add_slot();
+      }
+    } catch (HipError&) {
+      return BLSGPU_DEVICE_ERROR;
+    }
   } else {
     return BLSGPU_ERR_ARGS;
   }
@@ -589,13 +662,17 @@ int blsgpu_verify(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, bl
   std::vector<blsgpu_stats> sst(shards.size());
   std::vector<int> rc(shards.size(), BLSGPU_OK);
   auto work = [&](size_t k) {
+    Device& d = *ctx->devs[k];
+    std::shared_lock<std::shared_mutex> tl(d.table_mu);
+    Slot* sl = d.acquire();
     try {
-      rc[k] = run_shard(ctx, *ctx->devs[k], *b, shards[k], job_result, seed, sst[k]);
+      rc[k] = run_shard(ctx, d, *sl, *b, shards[k], job_result, seed, sst[k]);
     } catch (HipError&) {
       rc[k] = BLSGPU_DEVICE_ERROR;
     } catch (...) {
       rc[k] = BLSGPU_DEVICE_ERROR;
     }
+    d.release(sl);
     if (rc[k] == BLSGPU_DEVICE_ERROR)
       for (uint32_t j = shards[k].job_begin; j < shards[k].job_end; j++) job_result[j] = -BLSGPU_DEVICE_ERROR;
   };
@@ -608,7 +685,7 @@ int blsgpu_verify(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, bl
   }
   auto t1 = std::chrono::steady_clock::now();
   int status = BLSGPU_OK;
-  for (int k = 0; k < 8; k++) local.stage_ms[k] = sst[0].stage_ms[k];
+  for (int k = 0; k < kStages; k++) local.stage_ms[k] = sst[0].stage_ms[k];
   for (size_t k = 0; k < shards.size(); k++) {
     local.groups += sst[k].groups;
     local.batch_retries += sst[k].batch_retries;
@@ -656,7 +733,10 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, bl
     o->b.set_pk_first = o->pkfirst.data();
     o->b.pk_index = o->pkidx.data();
   }
-  ctx->inflight++;
+  {
+    std::lock_guard<std::mutex> lk(ctx->async_mu);
+    ctx->inflight++;
+  }
   std::thread([ctx, o, job_result, stats, done, user]() {
     int rc = ctx->closed ? BLSGPU_ERR_CLOSED : blsgpu_verify(ctx, &o->b, job_result, stats);
     delete o;
@@ -696,9 +776,10 @@ int blsgpu_debug_op(blsgpu_ctx* ctx, int op, uint32_t n, const uint8_t* in, uint
   if (!ctx || ctx->devs.empty() || !in || !out || !status) return BLSGPU_ERR_ARGS;
   if (n == 0) return BLSGPU_OK;
   Device* d = ctx->devs[0];
-  std::lock_guard<std::mutex> lk(d->mu);
+  Slot* sl = d->acquire();
   uint8_t *din = nullptr, *dout = nullptr;
   int32_t* dst = nullptr;
+  int rc = BLSGPU_OK;
   try {
     HIPCHK(hipSetDevice(d->id));
     HIPCHK(hipMalloc((void**)&din, (size_t)n * in_stride));
@@ -706,21 +787,19 @@ int blsgpu_debug_op(blsgpu_ctx* ctx, int op, uint32_t n, const uint8_t* in, uint
     HIPCHK(hipMalloc((void**)&dst, (size_t)n * 4));
     HIPCHK(hipMemcpy(din, in, (size_t)n * in_stride, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(dout, 0, (size_t)n * out_stride));
-    launch_debug_op(op, n, din, in_stride, dout, out_stride, dst, d->stream);
+    launch_debug_op(op, n, din, in_stride, dout, out_stride, dst, sl->stream);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(d->stream));
+    HIPCHK(hipStreamSynchronize(sl->stream));
     HIPCHK(hipMemcpy(out, dout, (size_t)n * out_stride, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(status, dst, (size_t)n * 4, hipMemcpyDeviceToHost));
   } catch (HipError&) {
-    if (din) (void)hipFree(din);
-    if (dout) (void)hipFree(dout);
-    if (dst) (void)hipFree(dst);
-    return BLSGPU_DEVICE_ERROR;
+    rc = BLSGPU_DEVICE_ERROR;
   }
-  (void)hipFree(din);
-  (void)hipFree(dout);
-  (void)hipFree(dst);
-  return BLSGPU_OK;
+  if (din) (void)hipFree(din);
+  if (dout) (void)hipFree(dout);
+  if (dst) (void)hipFree(dst);
+  d->release(sl);
+  return rc;
 }
 
 }  // extern "C"

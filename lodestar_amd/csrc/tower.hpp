@@ -131,7 +131,7 @@ BLS_FN fp6 fp6_mul_by_1(const fp6& x, const fp2& l1) {
   return fp6_make(fp2_mul_xi(fp2_mul(x.c2, l1)), fp2_mul(x.c0, l1), fp2_mul(x.c1, l1));
 }
 
-BLS_FN fp6 fp6_inv(const fp6& a) {
+BLS_BIG fp6 fp6_inv(const fp6& a) {
   fp2 t0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
   fp2 t1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
   fp2 t2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
@@ -168,7 +168,7 @@ BLS_FN fp12 fp12_sqr(const fp12& a) {
 
 BLS_HD fp12 fp12_conj(const fp12& a) { return fp12_make(a.c0, fp6_neg(a.c1)); }
 
-BLS_FN fp12 fp12_inv(const fp12& a) {
+BLS_BIG fp12 fp12_inv(const fp12& a) {
   fp6 t = fp6_sub(fp6_mul(a.c0, a.c0), fp6_mul_v(fp6_mul(a.c1, a.c1)));
   fp6 ti = fp6_inv(t);
   return fp12_make(fp6_mul(a.c0, ti), fp6_neg(fp6_mul(a.c1, ti)));
@@ -206,7 +206,7 @@ BLS_FN fp12 fp12_frob2(const fp12& a) {
   return r;
 }
 
-BLS_FN bool fp12_is_one(const fp12& a) {
+BLS_BIG bool fp12_is_one(const fp12& a) {
   bool r = fp2_eq(a.c0.c0, fp2_one());
   r = r && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2);
   r = r && fp2_is_zero(a.c1.c0) && fp2_is_zero(a.c1.c1) && fp2_is_zero(a.c1.c2);
