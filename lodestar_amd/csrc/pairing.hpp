@@ -80,11 +80,12 @@ BLS_HDNI fp12 miller_loop(const g1a& P, const g2a& Q) {
   return fp12_conj(f);
 }
 
-// f^|z| (plain square-and-multiply; f in the cyclotomic subgroup after the easy part)
+// f^|z| by square-and-multiply with cyclotomic squarings (f is in the cyclotomic subgroup: only called
+// after the easy part of the final exponentiation)
 BLS_HDNI fp12 fp12_pow_zabs(const fp12& f) {
   fp12 r = f;
   for (int i = 62; i >= 0; i--) {
-    r = fp12_sqr(r);
+    r = fp12_cyclotomic_sqr(r);
     if ((BLS_Z_ABS >> i) & 1ull) r = fp12_mul(r, f);
   }
   return r;

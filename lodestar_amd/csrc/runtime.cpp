@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+#include <stdlib.h>
 #include <sys/random.h>
 
 #include <algorithm>
@@ -481,6 +482,10 @@ extern "C" {
 int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
   if (!out) return BLSGPU_ERR_ARGS;
   *out = nullptr;
+  // Every slot needs its own hardware queue: kernels of streams that share one run in order, and a
+  // batch's single-wave tail (k_group_check) would then block the next batch's stage kernels.  HIP reads
+  // this once, at its initialization; an explicit setting by the user wins.
+  setenv("GPU_MAX_HW_QUEUES", "16", 0);
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return BLSGPU_ERR_NO_DEVICE;
   std::vector<int> ids;

@@ -184,6 +184,38 @@ BLS_FN fp12 fp12_mul_by_014(const fp12& f, const fp2& l0, const fp2& l1, const f
   return fp12_make(c0, c1);
 }
 
+// Squaring in the cyclotomic subgroup (Granger-Scott, eprint 2009/565 section 3.2): f^(p^6+1) = 1 lets
+// f^2 be computed from three Fp4 squarings -- 9 Fp2 squarings (18 Fp products) instead of 36.
+// Only valid after the easy part of the final exponentiation.
+BLS_INL void fp4_sqr(const fp2& a, const fp2& b, fp2& c0, fp2& c1) {
+  fp2 t0 = fp2_sqr(a);
+  fp2 t1 = fp2_sqr(b);
+  c0 = fp2_add(fp2_mul_xi(t1), t0);
+  c1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
+}
+BLS_INL fp2 cyc_fix_sub(const fp2& t, const fp2& z) {  // 2 (t - z) + t = 3t - 2z
+  fp2 d = fp2_sub(t, z);
+  return fp2_add(fp2_dbl(d), t);
+}
+BLS_INL fp2 cyc_fix_add(const fp2& t, const fp2& z) {  // 2 (t + z) + t = 3t + 2z
+  fp2 d = fp2_add(t, z);
+  return fp2_add(fp2_dbl(d), t);
+}
+BLS_INL fp12 fp12_cyclotomic_sqr(const fp12& f) {
+  fp2 t0, t1, t2, t3, u0, u1;
+  fp4_sqr(f.c0.c0, f.c1.c1, t0, t1);
+  fp12 r;
+  r.c0.c0 = cyc_fix_sub(t0, f.c0.c0);
+  r.c1.c1 = cyc_fix_add(t1, f.c1.c1);
+  fp4_sqr(f.c1.c0, f.c0.c2, u0, u1);
+  fp4_sqr(f.c0.c1, f.c1.c2, t2, t3);
+  r.c0.c1 = cyc_fix_sub(u0, f.c0.c1);
+  r.c1.c2 = cyc_fix_add(u1, f.c1.c2);
+  r.c1.c0 = cyc_fix_add(fp2_mul_xi(t3), f.c1.c0);
+  r.c0.c2 = cyc_fix_sub(t2, f.c0.c2);
+  return r;
+}
+
 // Frobenius x -> x^(p^k) for k = 1, 2, 3
 BLS_FN fp12 fp12_frob1(const fp12& a) {
   fp12 r;

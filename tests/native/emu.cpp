@@ -161,5 +161,6 @@ void emu_final_exp(const uint8_t* f576, uint8_t* out576) { store12(final_exponen
 void emu_fp12_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { store12(fp12_mul(load12(a), load12(b)), out); }
 void emu_fp12_sqr(const uint8_t* a, uint8_t* out) { store12(fp12_sqr(load12(a)), out); }
 void emu_fp12_inv(const uint8_t* a, uint8_t* out) { store12(fp12_inv(load12(a)), out); }
+void emu_fp12_cyc_sqr(const uint8_t* a, uint8_t* out) { store12(fp12_cyclotomic_sqr(load12(a)), out); }
 void emu_fp12_frob1(const uint8_t* a, uint8_t* out) { store12(fp12_frob1(load12(a)), out); }
 }

@@ -78,6 +78,11 @@ def test_fp12_ops():
         assert b2f12(o.raw) == bls.f12inv(a)
         L.emu_fp12_frob1(f12b(a), o)
         assert b2f12(o.raw) == bls.f12frob(a, 1)
+        # cyclotomic squaring agrees with plain squaring on the cyclotomic subgroup (after the easy part)
+        c = bls.f12mul(bls.f12conj(a), bls.f12inv(a))
+        c = bls.f12mul(bls.f12frob(c, 2), c)
+        L.emu_fp12_cyc_sqr(f12b(c), o)
+        assert b2f12(o.raw) == bls.f12sqr(c)
 
 
 def test_expand_and_hash_to_field():
