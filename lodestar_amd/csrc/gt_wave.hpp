@@ -1,0 +1,514 @@
+// Workgroup-cooperative GT (Fp12) arithmetic for the latency-bound tail of a batch check.
+//
+// The per-group tail -- one Miller loop for (-g1, S) and one final exponentiation -- is a single serial
+// chain per batch group, so lane-per-group code leaves 127 of 128 lanes of its workgroup idle and runs
+// ~15k Montgomery products back to back.  Here one 128-lane workgroup owns one group and every Fp12
+// operation is split into its independent Fp products, one per lane, so the chain's depth drops from
+// ~36-54 products per Fp12 operation to ~1 product plus a lazily reduced recombination:
+//   * Fp12 values live in LDS in the w-basis (Fp12 = Fp2[w]/(w^6 - xi), xi = 1 + u): coefficient k of
+//     w^k is (c0.c0, c1.c0, c0.c1, c1.c1, c0.c2, c1.c2)[k] of the tower layout, Fp index q = 2k + comp;
+//   * a product phase: lane t computes one Fp product (Karatsuba components of the Fp2 pair products) into
+//     the scratch S; a recombination phase: 12 lanes each form one output Fp component as a signed sum of
+//     products, accumulated unreduced (lacc) and reduced once;
+//   * serial leftovers (two inversions, five Miller addition steps) run on lane 0 with the register code
+//     of tower.hpp / pairing.hpp.
+// Same algorithm (operation for operation) as pairing.hpp's miller_loop / final_exponentiation, which the
+// oracle pins; tests/test_gpu_pipeline.py compares both against oracle/bls12_381.py.
+#pragma once
+#include "pairing.hpp"
+
+#define GTW_LANES 128
+#define GTW_FP12 (12 * BLS_NL)
+
+// ---------------------------------------------------------------------------------------------------
+// Lazily reduced signed sums of Fp values (each <= 2p, normalized limbs): limb sums without carries,
+// one carry pass and one quotient-estimate reduction at the end.  At most 15 terms per side.
+// ---------------------------------------------------------------------------------------------------
+struct lacc {
+  uint32_t pos[BLS_NL], neg[BLS_NL];
+};
+BLS_INL void lacc_init(lacc& a) {
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) a.pos[i] = a.neg[i] = 0;
+}
+BLS_INL void lacc_add(lacc& a, const fp& x) {
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) a.pos[i] += x.l[i];
+}
+BLS_INL void lacc_sub(lacc& a, const fp& x) {
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) a.neg[i] += x.l[i];
+}
+// 32 p in 28-bit limbs
+BLS_INL uint32_t fp_p32_limb(int i) {
+  uint32_t lo = (FP_P.l[i] << 5) & BLS_MASK;
+  if (i == BLS_NL - 1) lo = FP_P.l[i] << 5;
+  return lo | (i ? (FP_P.l[i - 1] >> (BLS_LB - 5)) : 0u);
+}
+// pos - neg (mod p), result <= 2p normalized
+BLS_INL fp lacc_fin(const lacc& a) {
+  uint32_t v[BLS_NL];
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    int64_t d = (int64_t)a.pos[i] + (int64_t)fp_p32_limb(i) - (int64_t)a.neg[i] + c;
+    if (i < BLS_NL - 1) {
+      v[i] = (uint32_t)d & BLS_MASK;
+      c = d >> BLS_LB;
+    } else {
+      v[i] = (uint32_t)d;  // value < 48 p < 2^387: top limb < 2^23
+    }
+  }
+  // q ~ floor(v / p), never above it and at most one below (p / 2^336 ~ 2^44.7: the 51-bit estimate's
+  // error is far below 1), so v - q p is in [0, 2p)
+  const double vhi = (double)v[BLS_NL - 1] * 268435456.0 + (double)v[BLS_NL - 2];
+  const double phi = (double)FP_P.l[BLS_NL - 1] * 268435456.0 + (double)FP_P.l[BLS_NL - 2] + 1.0;
+  const uint32_t q = (uint32_t)(vhi / phi);
+  fp r;
+  c = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    int64_t d = (int64_t)v[i] - (int64_t)((uint64_t)q * FP_P.l[i]) + c;
+    if (i < BLS_NL - 1) {
+      r.l[i] = (uint32_t)d & BLS_MASK;
+      c = d >> BLS_LB;
+    } else {
+      r.l[i] = (uint32_t)d;
+    }
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// LDS access (Fp index q of a buffer: words q*14 .. q*14+13)
+// ---------------------------------------------------------------------------------------------------
+BLS_INL fp lds_ld(const uint32_t* b, int q) {
+  fp r;
+#pragma unroll
+  for (int l = 0; l < BLS_NL; l++) r.l[l] = b[q * BLS_NL + l];
+  return r;
+}
+BLS_INL void lds_st(uint32_t* b, int q, const fp& v) {
+#pragma unroll
+  for (int l = 0; l < BLS_NL; l++) b[q * BLS_NL + l] = v.l[l];
+}
+BLS_INL void gtw_sync() { __syncthreads(); }
+
+// (x0 + x1 u)^2 = (x0 + x1)(x0 - x1) + (2 x0) x1 u : operands of component `comp`'s single product
+BLS_INL void sqr_operands(const fp& x0, const fp& x1, int comp, fp& X, fp& Y) {
+  X = comp ? fp_add_nr(x0, x0) : fp_add_nr(x0, x1);
+  Y = comp ? x1 : fp_sub(x0, x1);
+}
+// Karatsuba component c of (a0 + a1 u)(b0 + b1 u): c0 = a0 b0, c1 = a1 b1, c2 = (a0 + a1)(b0 + b1)
+BLS_INL void kara_operands(const fp& a0, const fp& a1, const fp& b0, const fp& b1, int c, fp& X, fp& Y) {
+  X = c == 0 ? a0 : (c == 1 ? a1 : fp_add_nr(a0, a1));
+  Y = c == 0 ? b0 : (c == 1 ? b1 : fp_add_nr(b0, b1));
+}
+
+// ---------------------------------------------------------------------------------------------------
+// C = A * B (C may alias A or B).  SPARSE: B is a Miller line with w-coefficients 0, 2, 3 only.
+// ---------------------------------------------------------------------------------------------------
+template <bool SPARSE>
+__device__ void gtw_mul(uint32_t* C, const uint32_t* A, const uint32_t* B, uint32_t* S, uint32_t t) {
+  constexpr uint32_t NP = SPARSE ? 54 : 108;
+  if (t < NP) {
+    const int pr = t / 3, c = t % 3;
+    int i, j;
+    if (SPARSE) {
+      i = pr / 3;
+      const int jj = pr % 3;
+      j = jj == 0 ? 0 : jj + 1;
+    } else {
+      i = pr / 6;
+      j = pr % 6;
+    }
+    fp X, Y;
+    kara_operands(lds_ld(A, 2 * i), lds_ld(A, 2 * i + 1), lds_ld(B, 2 * j), lds_ld(B, 2 * j + 1), c, X, Y);
+    lds_st(S, t, fp_mul(X, Y));
+  }
+  gtw_sync();
+  if (t < 12) {
+    const int k = t >> 1, comp = t & 1;
+    lacc acc;
+    lacc_init(acc);
+#pragma unroll 1
+    for (int i = 0; i < 6; i++) {
+      const int j = (k - i + 6) % 6;
+      const bool tw = i > k;  // i + j >= 6: the product carries w^6 = xi
+      int pr;
+      if (SPARSE) {
+        if (j == 1 || j > 3) continue;
+        pr = i * 3 + (j == 0 ? 0 : j - 1);
+      } else {
+        pr = i * 6 + j;
+      }
+      const fp P0 = lds_ld(S, 3 * pr), P1 = lds_ld(S, 3 * pr + 1), P2 = lds_ld(S, 3 * pr + 2);
+      // product = (P0 - P1) + (P2 - P0 - P1) u ; times xi: (2 P0 - P2) + (P2 - 2 P1) u
+      if (comp == 0) {
+        lacc_add(acc, P0);
+        if (tw) {
+          lacc_add(acc, P0);
+          lacc_sub(acc, P2);
+        } else {
+          lacc_sub(acc, P1);
+        }
+      } else {
+        lacc_add(acc, P2);
+        lacc_sub(acc, P1);
+        if (tw)
+          lacc_sub(acc, P1);
+        else
+          lacc_sub(acc, P0);
+      }
+    }
+    lds_st(C, t, lacc_fin(acc));
+  }
+  gtw_sync();
+}
+
+// ---------------------------------------------------------------------------------------------------
+// D = A^2 in the cyclotomic subgroup (Granger-Scott, as fp12_cyclotomic_sqr in tower.hpp): the w-pairs
+// (k, k+3) are Fp4 elements; 9 Fp2 squarings = 18 Fp products, then 12 recombination lanes.
+// ---------------------------------------------------------------------------------------------------
+__device__ void gtw_cyc_sqr(uint32_t* D, const uint32_t* A, uint32_t* S, uint32_t t) {
+  if (t < 18) {
+    const int p = t / 6, sq = (t % 6) >> 1, comp = t & 1;
+    fp x0, x1;
+    if (sq == 0) {
+      x0 = lds_ld(A, 2 * p);
+      x1 = lds_ld(A, 2 * p + 1);
+    } else if (sq == 1) {
+      x0 = lds_ld(A, 2 * p + 6);
+      x1 = lds_ld(A, 2 * p + 7);
+    } else {
+      x0 = fp_add(lds_ld(A, 2 * p), lds_ld(A, 2 * p + 6));
+      x1 = fp_add(lds_ld(A, 2 * p + 1), lds_ld(A, 2 * p + 7));
+    }
+    fp X, Y;
+    sqr_operands(x0, x1, comp, X, Y);
+    lds_st(S, t, fp_mul(X, Y));
+  }
+  gtw_sync();
+  if (t < 12) {
+    const int k = t >> 1, comp = t & 1;
+    // output k: pair, kind (0: c0 = xi t1 + t0, 1: c1 = s^2 - t0 - t1, 2: xi c1), sign of the 2 f_k term
+    const int p = (k == 0 || k == 3) ? 0 : ((k == 2 || k == 5) ? 1 : 2);
+    const int kind = (k == 0 || k == 2 || k == 4) ? 0 : (k == 1 ? 2 : 1);
+    const fp t0r = lds_ld(S, 6 * p), t0i = lds_ld(S, 6 * p + 1);
+    const fp t1r = lds_ld(S, 6 * p + 2), t1i = lds_ld(S, 6 * p + 3);
+    const fp sr = lds_ld(S, 6 * p + 4), si = lds_ld(S, 6 * p + 5);
+    lacc acc;
+    lacc_init(acc);
+#pragma unroll
+    for (int rep = 0; rep < 3; rep++) {
+      if (kind == 0) {
+        // c0 = (t1r - t1i + t0r) + (t1r + t1i + t0i) u
+        lacc_add(acc, t1r);
+        if (comp == 0) {
+          lacc_sub(acc, t1i);
+          lacc_add(acc, t0r);
+        } else {
+          lacc_add(acc, t1i);
+          lacc_add(acc, t0i);
+        }
+      } else if (kind == 1) {
+        // c1 = (sr - t0r - t1r) + (si - t0i - t1i) u
+        lacc_add(acc, comp ? si : sr);
+        lacc_sub(acc, comp ? t0i : t0r);
+        lacc_sub(acc, comp ? t1i : t1r);
+      } else {
+        // xi c1 = (c1r - c1i) + (c1r + c1i) u
+        lacc_add(acc, sr);
+        lacc_sub(acc, t0r);
+        lacc_sub(acc, t1r);
+        if (comp == 0) {
+          lacc_sub(acc, si);
+          lacc_add(acc, t0i);
+          lacc_add(acc, t1i);
+        } else {
+          lacc_add(acc, si);
+          lacc_sub(acc, t0i);
+          lacc_sub(acc, t1i);
+        }
+      }
+    }
+    // cyc_fix_sub: 3 t - 2 z (outputs 0, 2, 4), cyc_fix_add: 3 t + 2 z (outputs 1, 3, 5)
+    const fp z = lds_ld(A, t);
+    if (k & 1) {
+      lacc_add(acc, z);
+      lacc_add(acc, z);
+    } else {
+      lacc_sub(acc, z);
+      lacc_sub(acc, z);
+    }
+    lds_st(D, t, lacc_fin(acc));
+  }
+  gtw_sync();
+}
+
+// elementwise: D = conj(A) (negate the odd w-coefficients) or a copy
+__device__ void gtw_conj(uint32_t* D, const uint32_t* A, uint32_t t, bool negate_odd = true) {
+  if (t < 12) {
+    const fp a = lds_ld(A, t);
+    lds_st(D, t, (negate_odd && ((t >> 1) & 1)) ? fp_neg(a) : a);
+  }
+  gtw_sync();
+}
+__device__ void gtw_copy(uint32_t* D, const uint32_t* A, uint32_t t) { gtw_conj(D, A, t, false); }
+
+BLS_INL fp2 frob_const(int e, int k) {
+  if (e == 1) {
+    switch (k) {
+      case 1: return FROB1_1;
+      case 2: return FROB1_2;
+      case 3: return FROB1_3;
+      case 4: return FROB1_4;
+      default: return FROB1_5;
+    }
+  }
+  switch (k) {
+    case 1: return FROB2_1;
+    case 2: return FROB2_2;
+    case 3: return FROB2_3;
+    case 4: return FROB2_4;
+    default: return FROB2_5;
+  }
+}
+// D = A^(p^e), e = 1 or 2 (as fp12_frob1 / fp12_frob2): coefficient k -> conj^e(a_k) * gamma_{e,k}
+__device__ void gtw_frob(uint32_t* D, const uint32_t* A, int e, uint32_t t) {
+  if (t < 12) {
+    const int k = t >> 1, comp = t & 1;
+    fp a0 = lds_ld(A, 2 * k), a1 = lds_ld(A, 2 * k + 1);
+    if (e == 1) a1 = fp_neg(a1);
+    fp r;
+    if (k == 0) {
+      r = comp ? a1 : a0;
+    } else {
+      const fp2 g = frob_const(e, k);
+      // re = a0 g0 - a1 g1 ; im = a0 g1 + a1 g0
+      const fp u = fp_mul(a0, comp ? g.c1 : g.c0);
+      const fp v = fp_mul(a1, comp ? g.c0 : g.c1);
+      r = comp ? fp_add(u, v) : fp_sub(u, v);
+    }
+    lds_st(D, t, r);
+  }
+  gtw_sync();
+}
+
+// ---------------------------------------------------------------------------------------------------
+// LDS <-> registers (lane-0 serial parts)
+// ---------------------------------------------------------------------------------------------------
+BLS_INL fp2* fp12_slot(fp12& f, int k) {
+  switch (k) {
+    case 0: return &f.c0.c0;
+    case 1: return &f.c1.c0;
+    case 2: return &f.c0.c1;
+    case 3: return &f.c1.c1;
+    case 4: return &f.c0.c2;
+    default: return &f.c1.c2;
+  }
+}
+__device__ fp12 gtw_to_reg(const uint32_t* A) {
+  fp12 f;
+#pragma unroll
+  for (int k = 0; k < 6; k++) *fp12_slot(f, k) = fp2_make(lds_ld(A, 2 * k), lds_ld(A, 2 * k + 1));
+  return f;
+}
+__device__ void gtw_from_reg(uint32_t* A, fp12 f) {
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    lds_st(A, 2 * k, fp12_slot(f, k)->c0);
+    lds_st(A, 2 * k + 1, fp12_slot(f, k)->c1);
+  }
+}
+__device__ void gtw_set_one(uint32_t* A, uint32_t t) {
+  if (t < 12) lds_st(A, t, t == 0 ? FP_ONE : fp_zero());
+  gtw_sync();
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Final exponentiation (same chain as pairing.hpp final_exponentiation; returns e^3).  F is consumed.
+// Work buffers: 5 Fp12 in W (W + GTW_FP12 * i).
+// ---------------------------------------------------------------------------------------------------
+__device__ void gtw_pow_z(uint32_t* Y, const uint32_t* X, uint32_t* S, uint32_t t) {
+  gtw_copy(Y, X, t);
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    gtw_cyc_sqr(Y, Y, S, t);
+    if ((BLS_Z_ABS >> i) & 1ull) gtw_mul<false>(Y, Y, X, S, t);
+  }
+  gtw_conj(Y, Y, t);  // z < 0
+}
+
+__device__ void gtw_final_exp(uint32_t* F, uint32_t* W, uint32_t* S, uint32_t t) {
+  uint32_t *U = W, *V = W + GTW_FP12, *M = W + 2 * GTW_FP12, *T = W + 3 * GTW_FP12, *X = W + 4 * GTW_FP12;
+  if (t == 0) gtw_from_reg(U, fp12_inv(gtw_to_reg(F)));
+  gtw_sync();
+  gtw_conj(V, F, t);
+  gtw_mul<false>(V, V, U, S, t);  // f1 = conj(f) / f
+  gtw_frob(U, V, 2, t);
+  gtw_mul<false>(M, U, V, S, t);  // m = f1^(p^2) f1
+  gtw_pow_z(U, M, S, t);
+  gtw_conj(V, M, t);
+  gtw_mul<false>(T, U, V, S, t);  // t = m^z conj(m)
+  gtw_pow_z(U, T, S, t);
+  gtw_conj(V, T, t);
+  gtw_mul<false>(T, U, V, S, t);  // t = t^z conj(t)
+  gtw_pow_z(U, T, S, t);
+  gtw_frob(V, T, 1, t);
+  gtw_mul<false>(T, U, V, S, t);  // t = t^z t^p
+  gtw_pow_z(U, T, S, t);
+  gtw_pow_z(X, U, S, t);
+  gtw_frob(V, T, 2, t);
+  gtw_mul<false>(X, X, V, S, t);
+  gtw_conj(V, T, t);
+  gtw_mul<false>(T, X, V, S, t);  // t = t^(z^2) t^(p^2) conj(t)
+  gtw_mul<false>(U, M, M, S, t);
+  gtw_mul<false>(U, U, M, S, t);
+  gtw_mul<false>(F, T, U, S, t);  // t m^3
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Miller loop f = conj(f_{|z|,Q}(P)) into F (as pairing.hpp miller_loop).  Q affine in LDS (QA: 4 Fp:
+// x.re, x.im, y.re, y.im), P = (xP, yP) uniform.  TB: T (6 Fp), then the doubling-step temporaries
+// (16 Fp).  L: an Fp12-layout line buffer (w-coefficients 0, 2, 3 used).
+// ---------------------------------------------------------------------------------------------------
+__device__ void gtw_dbl_step(uint32_t* TB, uint32_t* L, const fp& xP, const fp& yP, uint32_t* S, uint32_t t) {
+  uint32_t* D = TB + 6 * BLS_NL;
+  // phase 1: x y (Karatsuba, 3), y^2 (2), z^2 (2), (y + z)^2 (2), x^2 (2)
+  if (t < 11) {
+    const fp x0 = lds_ld(TB, 0), x1 = lds_ld(TB, 1), y0 = lds_ld(TB, 2), y1 = lds_ld(TB, 3);
+    const fp z0 = lds_ld(TB, 4), z1 = lds_ld(TB, 5);
+    fp X, Y;
+    if (t < 3) {
+      kara_operands(x0, x1, y0, y1, t, X, Y);
+    } else if (t < 5) {
+      sqr_operands(y0, y1, t - 3, X, Y);
+    } else if (t < 7) {
+      sqr_operands(z0, z1, t - 5, X, Y);
+    } else if (t < 9) {
+      sqr_operands(fp_add(y0, z0), fp_add(y1, z1), t - 7, X, Y);
+    } else {
+      sqr_operands(x0, x1, t - 9, X, Y);
+    }
+    lds_st(S, t, fp_mul(X, Y));
+  }
+  gtw_sync();
+  // phase 2 (component lanes): A = xy/2, E = 12 xi C, F = 3E, G = (B + F)/2, H = (y+z)^2 - B - C, 3J,
+  // B - F, l0 = E - B.  D slots (Fp2): 0 A, 1 B-F, 2 G, 3 E, 4 B, 5 H, 6 3J
+  if (t < 2) {
+    const int c = t;
+    const fp P0 = lds_ld(S, 0), P1 = lds_ld(S, 1), P2 = lds_ld(S, 2);
+    const fp Axy = c ? fp_sub(fp_sub(P2, P0), P1) : fp_sub(P0, P1);
+    const fp B = lds_ld(S, 3 + c);
+    const fp C0 = lds_ld(S, 5), C1 = lds_ld(S, 6);
+    const fp xiC = c ? fp_add(C0, C1) : fp_sub(C0, C1);
+    const fp E = fp_mul4(fp_mul3(xiC));
+    const fp F = fp_mul3(E);
+    const fp G = fp_half(fp_add(B, F));
+    const fp H = fp_sub(fp_sub(lds_ld(S, 7 + c), B), lds_ld(S, 5 + c));
+    lds_st(D, 0 + c, fp_half(Axy));
+    lds_st(D, 2 + c, fp_sub(B, F));
+    lds_st(D, 4 + c, G);
+    lds_st(D, 6 + c, E);
+    lds_st(D, 8 + c, B);
+    lds_st(D, 10 + c, H);
+    lds_st(D, 12 + c, fp_mul3(lds_ld(S, 9 + c)));
+    lds_st(L, 0 + c, fp_sub(E, B));  // l0 at w^0
+  }
+  gtw_sync();
+  // phase 3: A (B - F) (3), G^2 (2), E^2 (2), B H (3), 3J xP (2), H yP (2)
+  if (t < 14) {
+    fp X, Y;
+    if (t < 3) {
+      kara_operands(lds_ld(D, 0), lds_ld(D, 1), lds_ld(D, 2), lds_ld(D, 3), t, X, Y);
+    } else if (t < 5) {
+      sqr_operands(lds_ld(D, 4), lds_ld(D, 5), t - 3, X, Y);
+    } else if (t < 7) {
+      sqr_operands(lds_ld(D, 6), lds_ld(D, 7), t - 5, X, Y);
+    } else if (t < 10) {
+      kara_operands(lds_ld(D, 8), lds_ld(D, 9), lds_ld(D, 10), lds_ld(D, 11), t - 7, X, Y);
+    } else if (t < 12) {
+      X = lds_ld(D, 12 + (t - 10));
+      Y = xP;
+    } else {
+      X = lds_ld(D, 10 + (t - 12));
+      Y = yP;
+    }
+    lds_st(S, t, fp_mul(X, Y));
+  }
+  gtw_sync();
+  // phase 4: T = (A(B-F), G^2 - 3E^2, B H), l1 = 3J xP at w^2, l4 = -H yP at w^3
+  if (t < 2) {
+    const int c = t;
+    const fp P0 = lds_ld(S, 0), P1 = lds_ld(S, 1), P2 = lds_ld(S, 2);
+    lds_st(TB, 0 + c, c ? fp_sub(fp_sub(P2, P0), P1) : fp_sub(P0, P1));
+    lds_st(TB, 2 + c, fp_sub(lds_ld(S, 3 + c), fp_mul3(lds_ld(S, 5 + c))));
+    const fp Q0 = lds_ld(S, 7), Q1 = lds_ld(S, 8), Q2 = lds_ld(S, 9);
+    lds_st(TB, 4 + c, c ? fp_sub(fp_sub(Q2, Q0), Q1) : fp_sub(Q0, Q1));
+    lds_st(L, 4 + c, lds_ld(S, 10 + c));
+    lds_st(L, 6 + c, fp_neg(lds_ld(S, 12 + c)));
+  }
+  gtw_sync();
+}
+
+__device__ void gtw_add_step(uint32_t* TB, const uint32_t* QA, uint32_t* L, const fp& xP, const fp& yP, uint32_t t) {
+  if (t == 0) {
+    g2proj T;
+    T.x = fp2_make(lds_ld(TB, 0), lds_ld(TB, 1));
+    T.y = fp2_make(lds_ld(TB, 2), lds_ld(TB, 3));
+    T.z = fp2_make(lds_ld(TB, 4), lds_ld(TB, 5));
+    g2a Q;
+    Q.x = fp2_make(lds_ld(QA, 0), lds_ld(QA, 1));
+    Q.y = fp2_make(lds_ld(QA, 2), lds_ld(QA, 3));
+    fp2 l0, l1, l4;
+    miller_add_step(T, Q, xP, yP, l0, l1, l4);
+    lds_st(TB, 0, T.x.c0);
+    lds_st(TB, 1, T.x.c1);
+    lds_st(TB, 2, T.y.c0);
+    lds_st(TB, 3, T.y.c1);
+    lds_st(TB, 4, T.z.c0);
+    lds_st(TB, 5, T.z.c1);
+    lds_st(L, 0, l0.c0);
+    lds_st(L, 1, l0.c1);
+    lds_st(L, 4, l1.c0);
+    lds_st(L, 5, l1.c1);
+    lds_st(L, 6, l4.c0);
+    lds_st(L, 7, l4.c1);
+  }
+  gtw_sync();
+}
+
+__device__ void gtw_miller_loop(uint32_t* F, const uint32_t* QA, const fp& xP, const fp& yP, uint32_t* TB, uint32_t* L,
+                                uint32_t* S, uint32_t t) {
+  if (t < 6) lds_st(TB, t, t < 4 ? lds_ld(QA, t) : (t == 4 ? FP_ONE : fp_zero()));
+  gtw_set_one(F, t);  // (syncs)
+  int bit = 62;
+  bool add_next = false;
+#pragma unroll 1
+  for (int s = 0; s < 68; s++) {
+    if (!add_next) {
+      if (s != 0) gtw_mul<false>(F, F, F, S, t);
+      gtw_dbl_step(TB, L, xP, yP, S, t);
+      add_next = (BLS_Z_ABS >> bit) & 1ull;
+      bit--;
+    } else {
+      gtw_add_step(TB, QA, L, xP, yP, t);
+      add_next = false;
+    }
+    gtw_mul<true>(F, F, L, S, t);
+  }
+  gtw_conj(F, F, t);
+}
+
+// LDS footprint of one cooperative group check (words)
+struct GtwLds {
+  uint32_t S[108 * BLS_NL];     // per-lane products
+  uint32_t F[GTW_FP12];         // accumulator
+  uint32_t G[GTW_FP12];         // Miller value
+  uint32_t W[5 * GTW_FP12];     // final-exponentiation temporaries
+  uint32_t L[GTW_FP12];         // line
+  uint32_t TB[(6 + 14) * BLS_NL];  // T + doubling temporaries
+  uint32_t QA[4 * BLS_NL];      // Q affine
+  uint32_t flag;
+};

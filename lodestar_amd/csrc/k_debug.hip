@@ -1,5 +1,6 @@
 // Element-wise test hooks behind blsgpu_debug_op (stage parity tests and workload generation).
 #include "k_common.hpp"
+#include "gt_wave.hpp"
 
 __device__ fp dbg_load_fp(const uint8_t* b) {
   fp x;
@@ -116,9 +117,48 @@ __global__ __launch_bounds__(WAVE) void k_debug_op(int op, uint32_t n, const uin
   status[i] = st;
 }
 
+// Workgroup-cooperative GT engine (gt_wave.hpp), one element per 128-lane block:
+//   op 16: final exponentiation of an Fp12 (576 B) -> Fp12
+//   op 17: Miller loop of (P: G1 affine 96 B, Q: G2 affine 192 B) -> Fp12
+__global__ __launch_bounds__(GTW_LANES) void k_debug_gt(int op, const uint8_t* in, uint32_t in_stride, uint8_t* out,
+                                                         uint32_t out_stride, int32_t* status) {
+  __shared__ GtwLds sh;
+  const uint32_t i = blockIdx.x, t = threadIdx.x;
+  const uint8_t* a = in + (size_t)i * in_stride;
+  uint8_t* o = out + (size_t)i * out_stride;
+  if (op == 16) {
+    if (t == 0) gtw_from_reg(sh.F, dbg_load_fp12(a));
+    gtw_sync();
+    gtw_final_exp(sh.F, sh.W, sh.S, t);
+  } else {
+    if (t == 0) {
+      const g1a P = dbg_load_g1(a);
+      const g2a Q = dbg_load_g2(a + 96);
+      lds_st(sh.QA, 0, Q.x.c0);
+      lds_st(sh.QA, 1, Q.x.c1);
+      lds_st(sh.QA, 2, Q.y.c0);
+      lds_st(sh.QA, 3, Q.y.c1);
+      lds_st(sh.L, 0, P.x);
+      lds_st(sh.L, 1, P.y);
+    }
+    gtw_sync();
+    const fp xP = lds_ld(sh.L, 0), yP = lds_ld(sh.L, 1);
+    gtw_sync();
+    gtw_miller_loop(sh.F, sh.QA, xP, yP, sh.TB, sh.L, sh.S, t);
+  }
+  if (t == 0) {
+    dbg_store_fp12(gtw_to_reg(sh.F), o);
+    status[i] = 0;
+  }
+}
+
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
 void launch_debug_op(int op, uint32_t n, const uint8_t* in, uint32_t in_stride, uint8_t* out, uint32_t out_stride,
                      int32_t* status, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_debug_op, grid_for(n), dim3(WAVE), 0, s, op, n, in, in_stride, out, out_stride, status);
+  if (!n) return;
+  if (op == 16 || op == 17)
+    hipLaunchKernelGGL(k_debug_gt, dim3(n), dim3(GTW_LANES), 0, s, op, in, in_stride, out, out_stride, status);
+  else
+    hipLaunchKernelGGL(k_debug_op, grid_for(n), dim3(WAVE), 0, s, op, n, in, in_stride, out, out_stride, status);
 }

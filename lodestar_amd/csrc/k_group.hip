@@ -5,10 +5,12 @@
 // The per-set Miller loops f_i were computed by k_miller_sets; here
 //   k_group_reduce   one wave per group: S = sum r_i sig_i (G2) and F = prod f_i (Fp12), each lane a strided
 //                    partial, then a 6-level LDS tree (64 -> 1)
-//   k_group_check    one lane per group: FinalExp(F * MillerLoop(-g1, S)) == 1
+//   k_group_check    one 128-lane workgroup per group: FinalExp(F * MillerLoop(-g1, S)) == 1, as
+//                    workgroup-cooperative Fp12 arithmetic (gt_wave.hpp)
 // The same two kernels re-check the sub-ranges of a failed group when the host bisects it
 // (runtime.cpp), so the fallback costs one Miller loop + final exponentiation per tested sub-range.
 #include "k_common.hpp"
+#include "gt_wave.hpp"
 
 // Lane per job: first error of the job, pubkeys before signatures (the reference deserializes pubkeys
 // first, worker.ts:39 / maybeBatch.ts:23), and the include mask of its sets.
@@ -61,19 +63,36 @@ __global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const 
   if (lane == 0) st_fp12(F_out, ng, g, F);
 }
 
-__global__ __launch_bounds__(WAVE) void k_group_check(const uint32_t* S_in, const uint32_t* F_in, uint32_t ng,
-                                                      uint8_t* ok) {
-  const uint32_t g = blockIdx.x * WAVE + threadIdx.x;
-  if (g >= ng) return;
-  fp12 f = ld_fp12(F_in, ng, g);
-  g2a Sa;
-  if (jac_to_aff(ld_g2j(S_in, ng, g), Sa)) {
-    g1a ng1;
-    ng1.x = G1_GEN_X;
-    ng1.y = G1_NEG_GEN_Y;
-    f = fp12_mul(f, miller_loop(ng1, Sa));
+// One 128-lane workgroup per group: the Miller loop and the final exponentiation run as cooperative Fp12
+// arithmetic (gt_wave.hpp), one Fp product per lane per step.
+__global__ __launch_bounds__(GTW_LANES) void k_group_check(const uint32_t* S_in, const uint32_t* F_in, uint32_t ng,
+                                                           uint8_t* ok) {
+  __shared__ GtwLds sh;
+  const uint32_t g = blockIdx.x, t = threadIdx.x;
+  // F: SoA tower layout (Fp2 slots c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2) -> LDS w-basis
+  for (uint32_t w = t; w < W_FP12; w += GTW_LANES) {
+    const uint32_t slot = w / (2 * W_FP), rest = w % (2 * W_FP);
+    const uint32_t k = slot < 3 ? 2 * slot : 2 * (slot - 3) + 1;
+    sh.F[k * 2 * W_FP + rest] = F_in[(size_t)w * ng + g];
   }
-  ok[g] = fp12_is_one(final_exponentiation(f)) ? 1 : 0;
+  if (t == 0) {
+    g2a Sa;
+    const bool fin = jac_to_aff(ld_g2j(S_in, ng, g), Sa);
+    if (fin) {
+      lds_st(sh.QA, 0, Sa.x.c0);
+      lds_st(sh.QA, 1, Sa.x.c1);
+      lds_st(sh.QA, 2, Sa.y.c0);
+      lds_st(sh.QA, 3, Sa.y.c1);
+    }
+    sh.flag = fin ? 1u : 0u;
+  }
+  gtw_sync();
+  if (sh.flag) {
+    gtw_miller_loop(sh.G, sh.QA, G1_GEN_X, G1_NEG_GEN_Y, sh.TB, sh.L, sh.S, t);
+    gtw_mul<false>(sh.F, sh.F, sh.G, sh.S, t);
+  }
+  gtw_final_exp(sh.F, sh.W, sh.S, t);
+  if (t == 0) ok[g] = fp12_is_one(gtw_to_reg(sh.F)) ? 1 : 0;
 }
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
@@ -86,5 +105,5 @@ void launch_group_reduce(const PipelineBuffers& b, const uint32_t* ranges, uint3
   if (ng) hipLaunchKernelGGL(k_group_reduce, dim3(ng), dim3(WAVE), 0, s, b, ranges, ng, S, F);
 }
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s) {
-  if (ng) hipLaunchKernelGGL(k_group_check, grid_for(ng), dim3(WAVE), 0, s, S, F, ng, ok);
+  if (ng) hipLaunchKernelGGL(k_group_check, dim3(ng), dim3(GTW_LANES), 0, s, S, F, ng, ok);
 }

@@ -84,6 +84,27 @@ def test_debug_miller_final_exp(ctx):
         assert b2f12(out2[576 * k : 576 * k + 576]) == bls.final_exp(f)
 
 
+def test_debug_gt_wave(ctx):
+    """Workgroup-cooperative Miller loop / final exponentiation (gt_wave.hpp, used by k_group_check) against
+    the oracle, including a Miller loop with an addition-heavy path (the 5 addition steps of |z|)."""
+    rnd = random.Random(5)
+    pts = [(bls.g1_mul(bls.G1_GEN, rnd.randrange(1, bls.R)), bls.g2_mul(bls.G2_GEN, rnd.randrange(1, bls.R)))
+           for _ in range(3)]
+    pts.append((bls.g1_neg(bls.G1_GEN), pts[0][1]))
+    out, st = ctx.debug_op(17, b"".join(g1b(p) + g2b(q) for p, q in pts), 288, 576)
+    assert (st == 0).all()
+    fs = []
+    for k, (p, q) in enumerate(pts):
+        f = b2f12(out[576 * k : 576 * k + 576])
+        assert f == bls.miller_loop(p, q), k
+        fs.append(f)
+    fs.append(bls.f12mul(fs[0], fs[1]))
+    out2, st2 = ctx.debug_op(16, b"".join(f12b(f) for f in fs), 576, 576)
+    assert (st2 == 0).all()
+    for k, f in enumerate(fs):
+        assert b2f12(out2[576 * k : 576 * k + 576]) == bls.final_exp(f), k
+
+
 def test_debug_scalar_mul(ctx):
     rnd = random.Random(11)
     Pp = bls.g1_mul(bls.G1_GEN, 99)
