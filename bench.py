@@ -8,7 +8,7 @@ sk_i = LE(sha256(LE32_32(i))) mod r (reference state-transition/src/util/interop
 device-resident table.  Inputs are generated on the GPU before timing (signing kernels) and are resident
 in host pinned staging; one step = one blsgpu_verify call = H2D + full verification + per-job results.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
 
 Prints one JSON line (rank 0).  Multi-GPU: each rank verifies its own 16,384 sets (weak scaling, no
@@ -53,7 +53,7 @@ def gen_sigs(ctx, sk_bytes_list, msgs):
     return sigs
 
 
-def build_workload(ctx, config, rank):
+def build_workload(ctx, config, rank, world=1):
     """Returns dict of numpy inputs for verify_raw + description."""
     if config == "C2":
         n = 16384
@@ -87,7 +87,107 @@ def build_workload(ctx, config, rank):
         desc = {"workload": "C3 block import: 128 aggregate sets x 512 pubkeys (GPU aggregation), one job",
                 "sets_per_step_per_gpu": n, "pubkeys_per_set": k, "pk_mode": "device table (65536 keys)"}
         return w, n, desc, k
+    if config == "C4":
+        return build_c4(ctx, rank, world)
+    if config == "C5":
+        return build_c5(ctx, rank)
     raise SystemExit(f"unknown config {config}")
+
+
+def _table_workload(ctx, set_idx, set_msg, set_sk, job_sizes, job_flags):
+    """Inputs for a table-mode call: set_idx[i] = pubkey indices of set i, set_sk[i] = its signing key."""
+    sigs = gen_sigs(ctx, [s.to_bytes(32, "big") for s in set_sk], set_msg)
+    n = len(set_idx)
+    spf = np.concatenate([[0], np.cumsum([len(x) for x in set_idx])]).astype(np.uint32)
+    return dict(job_first_set=np.concatenate([[0], np.cumsum(job_sizes)]).astype(np.uint32),
+                sigs=np.frombuffer(sigs, np.uint8), sig_len=np.full(n, 96, np.uint32),
+                msgs=np.frombuffer(b"".join(set_msg), np.uint8), set_pk_first=spf,
+                pk_index=np.concatenate([np.asarray(x, np.uint32) for x in set_idx]),
+                job_flags=np.asarray(job_flags, np.uint8), sig_stride=96)
+
+
+def build_c4(ctx, rank, world):
+    """C4 epoch scale: 2^20-validator table (replicated per GPU), 2,048 committees x 16 aggregate
+    sets = 32,768 sets, committee = 512 indices with a seed-random 0-10% dropout per set, one message per
+    committee, one batchable job per set.  The 32,768 sets are sharded over the ranks by
+    lodestar_amd.shard.shard_jobs (strong scaling)."""
+    from lodestar_amd.shard import shard_jobs
+
+    n_val, n_comm, per_comm, csize = 1 << 20, 2048, 16, 512
+    sk_all = [interop_sk(i) for i in range(4096)]  # keypairsMod-style tiling (reference perf util.ts:49-50)
+    sks_b = b"".join(s.to_bytes(32, "big") for s in sk_all)
+    pks, st = ctx.debug_op(8, sks_b, 32, 96)
+    assert (st == 0).all()
+    reps = n_val // 4096
+    for r in range(reps):  # validator i has key i mod 4096
+        ctx.upload_pubkeys(r * 4096, pks)
+    rng = np.random.default_rng(SEED)
+    perm = rng.permutation(n_val).astype(np.uint32)
+    n_sets = n_comm * per_comm
+    jfs_all = np.arange(n_sets + 1, dtype=np.uint32)
+    j0, j1 = shard_jobs(jfs_all, world, None)[rank]
+    set_idx, set_msg, set_sk = [], [], []
+    for s in range(n_sets):
+        c = s // per_comm
+        members = perm[(c * csize) % n_val : (c * csize) % n_val + csize]
+        drop = rng.random(csize) < rng.random() * 0.10
+        if not (j0 <= s < j1):
+            continue
+        idx = members[~drop] if (~drop).any() else members[:1]
+        set_idx.append(idx)
+        set_msg.append(msg_j(c))
+        set_sk.append(sum(sk_all[int(i) % 4096] for i in idx) % R_ORDER)
+    n = len(set_idx)
+    w = _table_workload(ctx, set_idx, set_msg, set_sk, [1] * n, [1] * n)
+    desc = {"workload": f"C4 epoch scale: 32768 aggregate sets (2048 committees x 16, 512-member committees, "
+                        f"0-10% dropout) over a 2^20-validator table, sharded {world} way(s)",
+            "sets_per_step_per_gpu": n, "total_sets_per_step": n_sets, "pubkeys_per_set": float(np.mean([len(x) for x in set_idx])),
+            "pk_mode": "device table (2^20 validators)", "distinct_messages": n_comm, "scaling": "strong"}
+    return w, n, desc, int(round(desc["pubkeys_per_set"]))
+
+
+def build_c5(ctx, rank):
+    """C5 mixed: 1,024 sets -- 25% proposer (single), 25% deposit-domain (single), 25%
+    sync-committee contribution (aggregate <= 128), 25% sync aggregate (aggregate 512) -- in batchable jobs of
+    1-3 sets, 1% of sets signed over the wrong message (-> false, invalid-batch fallback path).  Returns the
+    expected per-job results in w['expected']."""
+    n_keys = 8192
+    sks = [interop_sk(i) for i in range(n_keys)]
+    pks, st = ctx.debug_op(8, b"".join(s.to_bytes(32, "big") for s in sks), 32, 96)
+    assert (st == 0).all()
+    ctx.upload_pubkeys(0, pks)
+    rng = np.random.default_rng(SEED + rank)
+    n = 1024
+    set_idx, set_msg, set_sk = [], [], []
+    bad = set(rng.choice(n, size=n // 100, replace=False).tolist())
+    for s in range(n):
+        kind = s % 4
+        if kind < 2:
+            idx = rng.integers(0, n_keys, 1)
+        elif kind == 2:
+            idx = rng.choice(n_keys, size=int(rng.integers(1, 129)), replace=False)
+        else:
+            idx = rng.choice(n_keys, size=512, replace=False)
+        m = msg_j(rank * n + s)
+        set_idx.append(idx.astype(np.uint32))
+        set_msg.append(m)
+        set_sk.append(sum(sks[int(i)] for i in idx) % R_ORDER)
+    sign_msgs = [msg_j(rank * n + s + 1_000_000) if s in bad else set_msg[s] for s in range(n)]
+    job_sizes = []
+    left = n
+    while left:
+        k = min(left, int(rng.integers(1, 4)))
+        job_sizes.append(k)
+        left -= k
+    w = _table_workload(ctx, set_idx, sign_msgs, set_sk, job_sizes, [1] * len(job_sizes))
+    w["msgs"] = np.frombuffer(b"".join(set_msg), np.uint8)
+    jfs = w["job_first_set"]
+    w["expected"] = np.array([0 if any(s in bad for s in range(jfs[j], jfs[j + 1])) else 1
+                              for j in range(len(job_sizes))], np.int8)
+    desc = {"workload": "C5 mixed proposer/deposit/sync-contribution/sync-aggregate sets, jobs of 1-3, 1% invalid",
+            "sets_per_step_per_gpu": n, "pubkeys_per_set": float(np.mean([len(x) for x in set_idx])),
+            "pk_mode": "device table (8192 keys)", "invalid_sets": len(bad), "jobs": len(job_sizes)}
+    return w, n, desc, int(round(desc["pubkeys_per_set"]))
 
 
 def stage_mults(n_sets, group_count, pubkeys_per_set):
@@ -193,13 +293,18 @@ def main():
     ctx = Context([local_rank])
     ctx.set_option("group_sets", args.group_sets)
     ctx.set_option("slots", max(1, args.inflight))
-    work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank)
+    work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world)
     call = dict(work)
+    expected = call.pop("expected", None)
+    if expected is None:
+        expected = np.ones(len(call["job_first_set"]) - 1, np.int8)
 
     def step(_=None):
         res, st = ctx.verify_raw(**call, seed=SEED)
-        if not (res == 1).all():
-            raise SystemExit(f"verification failed on valid workload: {np.unique(res, return_counts=True)}")
+        if not np.array_equal(res, expected):
+            bad = np.nonzero(res != expected)[0]
+            raise SystemExit(f"verification mismatch on {len(bad)} jobs (first {bad[:8]}: got {res[bad[:8]]}, "
+                             f"want {expected[bad[:8]]})")
         return st
 
     pool = ThreadPoolExecutor(max_workers=max(1, args.inflight))  # ctypes releases the GIL inside the call
@@ -225,13 +330,11 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     groups = stats[-1].groups
-    if dist is not None:
-        import torch
+    from lodestar_amd.shard import max_over_ranks
 
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    total_sets = n_sets * args.steps * world
+    dt = max_over_ranks(dt, dist)
+    strong = desc.pop("scaling", "weak") == "strong"
+    total_sets = (desc["total_sets_per_step"] if strong else n_sets * world) * args.steps
     value = total_sets / dt
     # ---- isolated batches (untimed): p50 latency of one call, and per-stage kernel times ----
     lat = []
@@ -248,7 +351,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(dt * 1e3 / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u32/u64 (28-bit-limb Montgomery integer arithmetic)",
         "data": "synthetic (interop keys, SHA-256 messages, signatures generated on the GPU before timing)",

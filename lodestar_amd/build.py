@@ -34,6 +34,7 @@ def up_to_date():
 
 def build(force=False, verbose=True):
     if not force and up_to_date():
+        build_node_addon(verbose=verbose)
         return LIB
     objs = []
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include")]
@@ -58,7 +59,34 @@ def build(force=False, verbose=True):
     subprocess.check_call(cmd)
     for o in objs:
         os.remove(o)
+    build_node_addon(verbose=verbose)
     return LIB
+
+
+NODE_DIR = os.path.join(PKG, "node")
+ADDON = os.path.join(NODE_DIR, "blsgpu_napi.node")
+NODE_INC = "/usr/include/node"
+
+
+def build_node_addon(force=False, verbose=True):
+    """The N-API addon (lodestar_amd/node/blsgpu_napi.c) the JS BlsGpuVerifier loads.  Plain gcc against the
+    system node headers; links libblsgpu.so from the package directory (rpath $ORIGIN/..).  Skipped when the
+    node headers are absent."""
+    src = os.path.join(NODE_DIR, "blsgpu_napi.c")
+    if not os.path.exists(os.path.join(NODE_INC, "node_api.h")):
+        if verbose:
+            print("node headers not found: N-API addon not built", flush=True)
+        return None
+    if not force and os.path.exists(ADDON) and os.path.getmtime(ADDON) >= max(
+            os.path.getmtime(src), os.path.getmtime(LIB), os.path.getmtime(os.path.join(ROOT, "include", "blsgpu.h"))):
+        return ADDON
+    cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-Wno-unused-parameter", "-shared", "-fPIC",
+           "-DNODE_GYP_MODULE_NAME=blsgpu_napi", "-I", NODE_INC, "-I", os.path.join(ROOT, "include"), src,
+           "-o", ADDON, "-L", PKG, "-l:libblsgpu.so", "-Wl,-rpath,$ORIGIN/.."]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    return ADDON
 
 
 if __name__ == "__main__":

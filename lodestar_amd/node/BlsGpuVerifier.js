@@ -1,0 +1,264 @@
+"use strict";
+/**
+ * BlsGpuVerifier: the IBlsVerifier drop-in (reference packages/beacon-node/src/chain/bls/interface.ts:20-46)
+ * over the blsgpu N-API addon.  It replaces BlsMultiThreadWorkerPool (multithread/index.ts) with the same
+ * observable behaviour:
+ *
+ *   - verifySignatureSets(sets, opts) -> Promise<boolean>: true iff every set is valid; false if a
+ *     well-formed set fails the pairing equation; rejects with "BLST_ERROR: <CODE>" when a signature
+ *     fails to deserialize (maybeBatch.ts:23,36 -> Signature.fromBytes throws; multithread.test.ts:93-100),
+ *     with "EMPTY_AGGREGATE_ARRAY" for an aggregate without pubkeys (utils.ts:11), and with the device
+ *     status for a device error (never `false`, index.ts:368-375).
+ *   - batchable jobs are buffered for up to MAX_BUFFER_WAIT_MS or until more than MAX_BUFFERED_SIGS sets
+ *     are waiting, then submitted together; every job keeps its own result (index.ts:41-57, 238-285).
+ *     Non-batchable jobs are submitted on the next macrotask, so a synchronous loop of calls coalesces
+ *     into one submission (index.ts:276-283).
+ *   - close() rejects buffered and queued jobs with QUEUE_ERROR_QUEUE_ABORTED (index.ts:176-197) and
+ *     destroys the device context.
+ *
+ * Pubkeys.  A set's pubkey (single) or each of its pubkeys (aggregate) is one of:
+ *   - a validator index (number) into the device table filled by uploadPubkeys() from index2pubkey
+ *     (state-transition/src/cache/pubkeyCache.ts:56-77) -- GPU aggregation, no main-thread
+ *     PublicKey.aggregate (utils.ts:5-16);
+ *   - an object registered with registerPubkey(obj, index) (a blst PublicKey, mapped by identity);
+ *   - 96 uncompressed affine bytes (Uint8Array), or an object with toBytes() returning them -- what the
+ *     pool sends to its workers today (index.ts:160); only for single sets.
+ * A submission is in table mode when all its sets are indexed, in bytes mode otherwise; a flush that mixes
+ * both is split into one submission per mode.
+ */
+const path = require("path");
+
+const addon = require(path.join(__dirname, "blsgpu_napi.node"));
+
+const MAX_BUFFERED_SIGS = 32; // multithread/index.ts:48
+const MAX_BUFFER_WAIT_MS = 100; // multithread/index.ts:57
+const QUEUE_ABORTED = "QUEUE_ERROR_QUEUE_ABORTED"; // util/queue/errors.ts QueueErrorCode.QUEUE_ABORTED
+const SIG_STRIDE = 192;
+
+// job codes (include/blsgpu.h enum blsgpu_code)
+const CODE_EMPTY_AGGREGATE = 9;
+const CODE_EMPTY_SET = 10;
+
+class QueueError extends Error {
+  constructor(type) {
+    super(type.code);
+    this.type = type;
+  }
+}
+
+const SignatureSetType = {single: "single", aggregate: "aggregate"}; // signatureSets.ts:5-8
+
+function jobError(code) {
+  const name = addon.codeName(code) || `BLSGPU_${code}`;
+  if (code === CODE_EMPTY_SET || code === CODE_EMPTY_AGGREGATE) return new Error(name);
+  return new Error(`BLST_ERROR: ${name}`);
+}
+
+class BlsGpuVerifier {
+  /**
+   * @param {{devices?: number[], groupSets?: number, seed?: number}} opts
+   * @param {{metrics?: object, logger?: object}} modules
+   */
+  constructor(opts = {}, modules = {}) {
+    this.ctx = addon.init(opts.devices || null);
+    if (opts.groupSets) addon.setOption(this.ctx, "group_sets", opts.groupSets);
+    this.seed = opts.seed || 0; // 0 = OS CSPRNG batch scalars; fixed only for comparison runs
+    this.metrics = modules.metrics || null;
+    this.closed = false;
+    this.bufferedJobs = null; // {jobs, sigCount, timeout}
+    this.queued = []; // non-batchable jobs waiting for the next macrotask
+    this.queuedTimer = null;
+    this.inflight = new Set();
+    this.pkIndexOf = new WeakMap();
+    this.stats = {submissions: 0, jobs: 0, sets: 0, groups: 0, batchRetries: 0, batchSigsSuccess: 0};
+  }
+
+  /** index2pubkey sync: entries [firstIndex, firstIndex + n) as 96-byte uncompressed affine encodings. */
+  uploadPubkeys(firstIndex, pk96) {
+    addon.uploadPubkeys(this.ctx, firstIndex, pk96);
+  }
+
+  registerPubkey(obj, index) {
+    this.pkIndexOf.set(obj, index);
+  }
+
+  get deviceCount() {
+    return addon.deviceCount(this.ctx);
+  }
+
+  /**
+   * IBlsVerifier.verifySignatureSets (interface.ts:20-43).
+   * @param {Array<{type: string, pubkey?: any, pubkeys?: any[], signingRoot: Uint8Array, signature: Uint8Array}>} sets
+   * @param {{batchable?: boolean, verifyOnMainThread?: boolean}} opts
+   * @returns {Promise<boolean>}
+   */
+  async verifySignatureSets(sets, opts = {}) {
+    if (this.closed) throw new QueueError({code: QUEUE_ABORTED});
+    if (this.metrics && this.metrics.bls && this.metrics.bls.aggregatedPubkeys) {
+      let n = 0;
+      for (const s of sets) if (s.type === SignatureSetType.aggregate) n += s.pubkeys.length;
+      this.metrics.bls.aggregatedPubkeys.inc(n);
+    }
+    const job = this.encodeJob(sets, opts);
+    const code = await new Promise((resolve, reject) => {
+      job.resolve = resolve;
+      job.reject = reject;
+      if (opts.batchable && !opts.verifyOnMainThread) {
+        if (!this.bufferedJobs) {
+          this.bufferedJobs = {jobs: [], sigCount: 0, timeout: setTimeout(() => this.flushBuffered(), MAX_BUFFER_WAIT_MS)};
+        }
+        this.bufferedJobs.jobs.push(job);
+        this.bufferedJobs.sigCount += job.sets.length;
+        if (this.bufferedJobs.sigCount > MAX_BUFFERED_SIGS) {
+          clearTimeout(this.bufferedJobs.timeout);
+          this.flushBuffered();
+        }
+      } else if (opts.verifyOnMainThread) {
+        // latency-critical (block proposal, interface.ts:8-17): no buffering at all
+        this.dispatch([job]);
+      } else {
+        this.queued.push(job);
+        if (!this.queuedTimer) {
+          this.queuedTimer = setTimeout(() => {
+            this.queuedTimer = null;
+            const jobs = this.queued.splice(0, this.queued.length);
+            this.dispatch(jobs);
+          }, 0);
+        }
+      }
+    });
+    if (code < 0) throw jobError(-code);
+    return code === 1;
+  }
+
+  /** IBlsVerifier.close (interface.ts:45). */
+  async close() {
+    if (this.closed) return;
+    this.closed = true;
+    const pending = [];
+    if (this.bufferedJobs) {
+      clearTimeout(this.bufferedJobs.timeout);
+      pending.push(...this.bufferedJobs.jobs);
+      this.bufferedJobs = null;
+    }
+    if (this.queuedTimer) clearTimeout(this.queuedTimer);
+    this.queuedTimer = null;
+    pending.push(...this.queued.splice(0, this.queued.length));
+    for (const job of pending) job.reject(new QueueError({code: QUEUE_ABORTED}));
+    // in-flight submissions complete (the device finishes them) before the context is freed
+    await Promise.allSettled(Array.from(this.inflight));
+    addon.close(this.ctx);
+  }
+
+  // ------------------------------------------------------------------------------------ internals
+  flushBuffered() {
+    const b = this.bufferedJobs;
+    this.bufferedJobs = null;
+    if (b && b.jobs.length) this.dispatch(b.jobs);
+  }
+
+  pkRef(pk) {
+    if (typeof pk === "number") return {index: pk};
+    if (pk instanceof Uint8Array) return {bytes: pk};
+    if (pk && typeof pk === "object") {
+      const idx = this.pkIndexOf.get(pk);
+      if (idx !== undefined) return {index: idx};
+      if (typeof pk.toBytes === "function") return {bytes: pk.toBytes()};
+    }
+    throw new TypeError("BlsGpuVerifier: pubkey must be an index, a registered object or 96 bytes");
+  }
+
+  encodeJob(sets, opts) {
+    const enc = [];
+    let allIndexed = true;
+    for (const s of sets) {
+      const refs = s.type === SignatureSetType.aggregate ? s.pubkeys.map((p) => this.pkRef(p)) : [this.pkRef(s.pubkey)];
+      for (const r of refs) if (r.index === undefined) allIndexed = false;
+      enc.push({refs, msg: s.signingRoot, sig: s.signature, aggregate: s.type === SignatureSetType.aggregate});
+    }
+    if (!allIndexed) {
+      for (const e of enc) {
+        if (e.aggregate || e.refs.length !== 1 || e.refs[0].bytes === undefined || e.refs[0].bytes.length !== 96) {
+          throw new TypeError("BlsGpuVerifier: aggregate sets need indexed pubkeys; byte pubkeys must be 96-byte uncompressed");
+        }
+      }
+    }
+    return {sets: enc, table: allIndexed, batchable: !!opts.batchable};
+  }
+
+  dispatch(jobs) {
+    const table = jobs.filter((j) => j.table);
+    const bytes = jobs.filter((j) => !j.table);
+    if (table.length) this.submit(table, true);
+    if (bytes.length) this.submit(bytes, false);
+  }
+
+  submit(jobs, tableMode) {
+    let nSets = 0;
+    let nPk = 0;
+    for (const j of jobs) {
+      nSets += j.sets.length;
+      for (const s of j.sets) nPk += s.refs.length;
+    }
+    const jobFirstSet = new Uint32Array(jobs.length + 1);
+    const jobFlags = new Uint8Array(jobs.length);
+    const msgs = new Uint8Array(32 * nSets);
+    const sigs = new Uint8Array(SIG_STRIDE * nSets);
+    const sigLen = new Uint32Array(nSets);
+    const req = {jobFirstSet, jobFlags, msgs, sigs, sigLen, sigStride: SIG_STRIDE, seed: this.seed};
+    let setPkFirst, pkIndex, pkBytes;
+    if (tableMode) {
+      setPkFirst = req.setPkFirst = new Uint32Array(nSets + 1);
+      pkIndex = req.pkIndex = new Uint32Array(Math.max(nPk, 1));
+    } else {
+      pkBytes = req.pkBytes = new Uint8Array(96 * nSets);
+    }
+    let i = 0;
+    let k = 0;
+    jobs.forEach((j, ji) => {
+      jobFirstSet[ji] = i;
+      jobFlags[ji] = j.batchable ? 1 : 0;
+      for (const s of j.sets) {
+        msgs.set(s.msg.subarray(0, 32), 32 * i);
+        const sl = s.sig.length;
+        sigLen[i] = sl; // 96 / 192, anything else -> BLST_INVALID_SIZE for this job
+        sigs.set(s.sig.subarray(0, Math.min(sl, SIG_STRIDE)), SIG_STRIDE * i);
+        if (tableMode) {
+          setPkFirst[i] = k;
+          for (const r of s.refs) pkIndex[k++] = r.index;
+        } else {
+          pkBytes.set(s.refs[0].bytes, 96 * i);
+        }
+        i++;
+      }
+    });
+    jobFirstSet[jobs.length] = nSets;
+    if (tableMode) setPkFirst[nSets] = k;
+
+    const p = addon.submit(this.ctx, req).then(
+      (out) => {
+        const st = this.stats;
+        st.submissions++;
+        st.jobs += jobs.length;
+        st.sets += nSets;
+        st.groups += out.groups;
+        st.batchRetries += out.batchRetries;
+        st.batchSigsSuccess += out.batchSigsSuccess;
+        const m = this.metrics && this.metrics.blsThreadPool;
+        if (m) {
+          if (m.batchRetries) m.batchRetries.inc(out.batchRetries);
+          if (m.batchSigsSuccess) m.batchSigsSuccess.inc(out.batchSigsSuccess);
+        }
+        jobs.forEach((j, ji) => j.resolve(out.results[ji]));
+      },
+      (err) => {
+        // call-level failure (device error, closed context): reject every job, never resolve false
+        for (const j of jobs) j.reject(err.code === QUEUE_ABORTED ? new QueueError({code: QUEUE_ABORTED}) : err);
+      }
+    );
+    this.inflight.add(p);
+    p.finally(() => this.inflight.delete(p));
+  }
+}
+
+module.exports = {BlsGpuVerifier, QueueError, SignatureSetType, MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, addon};

@@ -1,0 +1,79 @@
+"""Multi-rank host logic on CPU (gloo, world_size 2): the job sharding every rank computes independently
+tiles the workload exactly once, is cost-balanced, never splits a job, and the bench's max-over-ranks timing
+rule holds.  No data-path collective exists; gloo carries only the checks."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from lodestar_amd.shard import job_costs, max_over_ranks, shard_jobs
+
+
+def workload(seed=7, n_jobs=997):
+    rng = np.random.default_rng(seed)
+    sets_per_job = rng.integers(0, 4, n_jobs)  # includes empty jobs
+    jfs = np.concatenate([[0], np.cumsum(sets_per_job)])
+    pks = rng.integers(1, 513, int(jfs[-1]))  # aggregate sizes up to a committee
+    spf = np.concatenate([[0], np.cumsum(pks)])
+    return jfs, spf
+
+
+def test_shard_jobs_single_process_properties():
+    jfs, spf = workload()
+    for n in (1, 2, 3, 8):
+        sh = shard_jobs(jfs, n, spf)
+        assert sh[0][0] == 0 and sh[-1][1] == len(jfs) - 1
+        assert all(a[1] == b[0] for a, b in zip(sh, sh[1:]))
+        cost = job_costs(jfs, spf)
+        per = [cost[b] - cost[a] for a, b in sh]
+        max_job = max(np.diff(cost))
+        assert max(per) - min(per) <= 2 * max_job + 1e-9
+    assert shard_jobs([0], 4) == [(0, 0)] * 4  # no jobs
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        jfs, spf = workload()
+        mine = shard_jobs(jfs, world, spf)[rank]
+        # every rank gathers every rank's independently computed range
+        got = [None] * world
+        dist.all_gather_object(got, mine)
+        dt = max_over_ranks(0.5 + rank)
+        q.put((rank, got, dt))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(120)
+def test_shard_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    jfs, spf = workload()
+    ranges = res[0][1]
+    assert all(r[1] == ranges for r in res)  # all ranks agree
+    covered = sorted(j for a, b in ranges for j in range(a, b))
+    assert covered == list(range(len(jfs) - 1))  # each job exactly once
+    assert all(r[2] == 1.5 for r in res)  # max over ranks
