@@ -234,13 +234,30 @@ def roofline(stage_ms_avg, n_sets, group_count, pubkeys_per_set, sets_per_s):
         "peak": round(VALU_PEAK_PRODUCTS / 1e12, 4),
         "unit": "T limb-products/s (32x32->64)",
         "frac": round(achieved * 1e12 / VALU_PEAK_PRODUCTS, 5),
-        "traffic": None,
+        "traffic": pmc_traffic(KERNEL_OF_STAGE[best], n_sets),
         "algorithmic_products_per_launch": mults[name] * ppm,
         "pipeline_products_per_step": total_products,
         "pipeline_achieved": round(pipe / 1e12, 4),
         "pipeline_frac": round(pipe / VALU_PEAK_PRODUCTS, 5),
         "stages": per_stage,
     }
+
+
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+PMC_SETS_PER_LAUNCH = 16384  # the C2 launch the counters were collected on (tools/gpurun/pmc.sh)
+
+
+def pmc_traffic(kernel, n_sets):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (FETCH_SIZE doubled for the
+    gfx950 half-count of wide reads, WRITE_SIZE as is; MI355X_MICROARCH.md HBM section), or None when the
+    counters were collected on a different launch size."""
+    if n_sets != PMC_SETS_PER_LAUNCH or not os.path.exists(PMC_FILE):
+        return None
+    with open(PMC_FILE) as fh:
+        k = json.load(fh)["kernels"].get(kernel)
+    if not k:
+        return None
+    return round(2 * 1024 * k["FETCH_SIZE_kB_per_launch"] + 1024 * k["WRITE_SIZE_kB_per_launch"])
 
 
 def cpu_baseline(work, n_sample=128, chunk=16):

@@ -40,6 +40,7 @@ struct PipelineBuffers {
   uint32_t* pk_aff;   // W_G1A (r * pk)
   uint32_t* rsig;     // W_G2J
   uint32_t* f;        // W_FP12
+  uint32_t* lines;    // Miller lines: MILLER_STEPS x 3 Fp2 (6 * W_FP words) per set, step-major SoA
   uint8_t* flags;     // [2n]: sig flags, hash flags
   int8_t* status;     // [2n]: signature status, pubkey status
   int8_t* job_err;    // [n_jobs]: first pubkey/signature error of the job (0 = clean)

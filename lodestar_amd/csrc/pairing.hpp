@@ -52,6 +52,73 @@ BLS_FN void miller_add_step(g2proj& T, const g2a& Q, const fp& xP, const fp& yP,
   T.z = Z3;
 }
 
+// ---- Two-pass Miller loop (pipeline form) -------------------------------------------------------------
+// Pass 1 (k_miller_lines) walks T over the 68 steps and emits each step's line in Q-only form
+// (l0, c1, c4) with l1 = c1 xP and l4 = c4 yP; pass 2 (k_miller_acc) folds the lines into f.  Splitting the
+// loop removes T/Q (and the line arithmetic) from the live state of the Fp12 accumulation, which is what
+// spilled to scratch in the one-pass loop (profiles/r01_pmc_traffic.json), and makes the lines depend on
+// H(m) only, so sets sharing a message can share them.  Same operations as miller_loop below.
+#define MILLER_STEPS 68
+struct line3 {
+  fp2 l0, c1, c4;
+};
+// step s of the flat loop is an addition step iff the previous doubling consumed a set bit of |z|
+BLS_HD bool miller_step_is_add(int s) {
+  int bit = 62;
+  bool add_next = false;
+  for (int k = 0; k < s; k++) {
+    if (!add_next) {
+      add_next = (BLS_Z_ABS >> bit) & 1ull;
+      bit--;
+    } else {
+      add_next = false;
+    }
+  }
+  return add_next;
+}
+BLS_FN void miller_dbl_line(g2proj& T, line3& L) {
+  fp2 A = fp2_half(fp2_mul(T.x, T.y));
+  fp2 B = fp2_sqr(T.y);
+  fp2 C = fp2_sqr(T.z);
+  fp2 E = fp2_mul3(fp2_mul_xi(C));
+  E = fp2_dbl(fp2_dbl(E));
+  fp2 F = fp2_mul3(E);
+  fp2 G = fp2_half(fp2_add(B, F));
+  fp2 H = fp2_sub(fp2_sub(fp2_sqr(fp2_add(T.y, T.z)), B), C);
+  fp2 J = fp2_sqr(T.x);
+  fp2 E2 = fp2_sqr(E);
+  T.x = fp2_mul(A, fp2_sub(B, F));
+  T.y = fp2_sub(fp2_sqr(G), fp2_mul3(E2));
+  T.z = fp2_mul(B, H);
+  L.l0 = fp2_sub(E, B);
+  L.c1 = fp2_mul3(J);
+  L.c4 = fp2_neg(H);
+}
+BLS_FN void miller_add_line(g2proj& T, const g2a& Q, line3& L) {
+  fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
+  fp2 lam = fp2_sub(T.x, fp2_mul(Q.x, T.z));
+  fp2 C = fp2_sqr(theta);
+  fp2 D = fp2_sqr(lam);
+  fp2 E = fp2_mul(lam, D);
+  fp2 F = fp2_mul(T.z, C);
+  fp2 G = fp2_mul(T.x, D);
+  fp2 H = fp2_sub(fp2_add(E, F), fp2_dbl(G));
+  fp2 X3 = fp2_mul(lam, H);
+  fp2 Y3 = fp2_sub(fp2_mul(theta, fp2_sub(G, H)), fp2_mul(T.y, E));
+  fp2 Z3 = fp2_mul(T.z, E);
+  L.l0 = fp2_sub(fp2_mul(theta, Q.x), fp2_mul(lam, Q.y));
+  L.c1 = fp2_neg(theta);
+  L.c4 = lam;
+  T.x = X3;
+  T.y = Y3;
+  T.z = Z3;
+}
+// f <- (s doubling && s > 0 ? f^2 : f) * line(P)
+BLS_FN fp12 miller_acc_step(const fp12& f, int s, bool is_add, const line3& L, const fp& xP, const fp& yP) {
+  fp12 g = (!is_add && s != 0) ? fp12_sqr(f) : f;
+  return fp12_mul_by_014(g, L.l0, fp2_mul_fp(L.c1, xP), fp2_mul_fp(L.c4, yP));
+}
+
 // f = conj(f_{|z|,Q}(P)).  P, Q affine and not infinity.
 // The 68 steps (63 doublings, 5 additions) run as one flat loop with a single copy of each step body:
 // a doubling step squares f first (except the very first), an addition step does not.

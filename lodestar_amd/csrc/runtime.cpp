@@ -87,6 +87,7 @@ struct HostBuf {  // pinned staging
 };
 
 constexpr int kStages = 8;
+constexpr size_t kMillerLineWords = 68 * 6 * W_FP;  // MILLER_STEPS x (l0, c1, c4) per set (k_miller.hip)
 
 // One in-flight batch on one device: a stream and every per-call buffer.
 struct Slot {
@@ -94,7 +95,7 @@ struct Slot {
   hipEvent_t ev[kStages + 1] = {};
   DevBuf<uint8_t> d_sigs, d_msgs, d_pkb, d_flags, d_ok, d_include;
   DevBuf<int8_t> d_status, d_joberr;
-  DevBuf<uint32_t> d_siglen, d_pkfirst, d_pkidx, d_jobs, d_ranges, d_work, d_S, d_F;
+  DevBuf<uint32_t> d_siglen, d_pkfirst, d_pkidx, d_jobs, d_ranges, d_work, d_S, d_F, d_lines;
   DevBuf<uint64_t> d_scalars;
   HostBuf<uint8_t> h_sigs, h_msgs, h_pkb, h_ok;
   HostBuf<int8_t> h_joberr;
@@ -104,7 +105,7 @@ struct Slot {
   void release_all() {
     d_sigs.release(); d_msgs.release(); d_pkb.release(); d_flags.release(); d_ok.release();
     d_include.release(); d_status.release(); d_joberr.release(); d_siglen.release(); d_pkfirst.release();
-    d_pkidx.release(); d_jobs.release(); d_ranges.release(); d_work.release(); d_S.release(); d_F.release();
+    d_pkidx.release(); d_jobs.release(); d_ranges.release(); d_work.release(); d_S.release(); d_F.release(); d_lines.release();
     d_scalars.release();
     h_sigs.release(); h_msgs.release(); h_pkb.release(); h_ok.release(); h_joberr.release();
     h_siglen.release(); h_pkfirst.release(); h_pkidx.release(); h_jobs.release(); h_ranges.release();
@@ -301,6 +302,7 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
   // work area: sig_aff, h_aff, pk_jac, pk_aff, rsig, f
   const size_t work_words = (size_t)stride * (W_G2A + W_G2A + W_G1J + W_G1A + W_G2J + W_FP12);
   sl.d_work.ensure(work_words);
+  sl.d_lines.ensure((size_t)stride * kMillerLineWords);
   hipStream_t s = sl.stream;
   HIPCHK(hipMemcpyAsync(sl.d_sigs.p, sl.h_sigs.p, (size_t)n * 192, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(sl.d_siglen.p, sl.h_siglen.p, (size_t)n * 4, hipMemcpyHostToDevice, s));
@@ -339,6 +341,7 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
   pb.pk_aff = w; w += (size_t)stride * W_G1A;
   pb.rsig = w; w += (size_t)stride * W_G2J;
   pb.f = w;
+  pb.lines = sl.d_lines.p;
   pb.flags = sl.d_flags.p;
   pb.status = sl.d_status.p;
   pb.job_err = sl.d_joberr.p;

@@ -157,6 +157,23 @@ int emu_g1_mul_u64(const uint8_t* p96, uint64_t k, uint8_t* out96) {
   return 1;
 }
 void emu_miller(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) { store12(miller_loop(load_g1(p96), load_g2(q192)), out576); }
+// two-pass form of the pipeline kernels (k_miller_lines + k_miller_acc)
+void emu_miller2(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) {
+  const g1a P = load_g1(p96);
+  const g2a Q = load_g2(q192);
+  static line3 L[MILLER_STEPS];
+  g2proj T;
+  T.x = Q.x;
+  T.y = Q.y;
+  T.z = fp2_one();
+  for (int s = 0; s < MILLER_STEPS; s++) {
+    if (miller_step_is_add(s)) miller_add_line(T, Q, L[s]);
+    else miller_dbl_line(T, L[s]);
+  }
+  fp12 f = fp12_one();
+  for (int s = 0; s < MILLER_STEPS; s++) f = miller_acc_step(f, s, miller_step_is_add(s), L[s], P.x, P.y);
+  store12(fp12_conj(f), out576);
+}
 void emu_final_exp(const uint8_t* f576, uint8_t* out576) { store12(final_exponentiation(load12(f576)), out576); }
 void emu_fp12_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { store12(fp12_mul(load12(a), load12(b)), out); }
 void emu_fp12_sqr(const uint8_t* a, uint8_t* out) { store12(fp12_sqr(load12(a)), out); }

@@ -137,6 +137,9 @@ def test_miller_and_final_exp():
     L.emu_miller(g1b(Pp), g2b(Q), o)
     f = b2f12(o.raw)
     assert f == bls.miller_loop(Pp, Q)
+    o3 = buf(576)
+    L.emu_miller2(g1b(Pp), g2b(Q), o3)  # two-pass pipeline form: lines of H(m), then the Fp12 fold
+    assert b2f12(o3.raw) == f
     o2 = buf(576)
     L.emu_final_exp(f12b(f), o2)
     assert b2f12(o2.raw) == bls.final_exp(f)
