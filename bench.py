@@ -283,11 +283,11 @@ def cpu_baseline(work, n_sample=128, chunk=16):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--group-sets", type=int, default=256)
-    ap.add_argument("--inflight", type=int, default=8,
+    ap.add_argument("--inflight", type=int, default=12,
                     help="verifySignatureSets calls in flight per GPU (runtime slots); 1 = strictly serial")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")

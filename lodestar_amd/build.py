@@ -11,7 +11,7 @@ import time
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
-LIB = os.path.join(PKG, "libblsgpu.so")
+LIB = os.environ.get("BLSGPU_LIB") or os.path.join(PKG, "libblsgpu.so")  # override: tuning variants
 ARCH = os.environ.get("BLSGPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["k_sig.hip", "k_hash.hip", "k_pk.hip", "k_miller.hip", "k_group.hip", "k_debug.hip", "runtime.cpp"]
@@ -38,11 +38,12 @@ def build(force=False, verbose=True):
         return LIB
     objs = []
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include")]
+    common += ["-D" + d for d in os.environ.get("BLSGPU_DEFINES", "").split()]  # e.g. BLSGPU_WPE=2
     # one translation unit per pipeline stage, compiled in parallel (the stage kernels are large)
     procs = []
     t0 = time.time()
     for src in SOURCES:
-        obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
+        obj = os.path.splitext(LIB)[0] + "." + os.path.splitext(src)[0] + ".o"
         objs.append(obj)
         cmd = [HIPCC] + common + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:

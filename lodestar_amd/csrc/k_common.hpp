@@ -7,6 +7,15 @@
 
 #define WAVE 64
 
+// Lane-per-set stage kernels.  BLSGPU_WPE is the number of waves per SIMD the register budget is sized for:
+// 1 lets a kernel take the whole 512-entry VGPR+AGPR file (no spills, but one resident wave per SIMD, so
+// concurrent batches cannot share a SIMD); 2 halves the budget so two in-flight batches co-reside and hide
+// each other's dependent-MAD latency, at the price of scratch spills.
+#ifndef BLSGPU_WPE
+#define BLSGPU_WPE 1
+#endif
+#define STAGE_KERNEL __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(BLSGPU_WPE, BLSGPU_WPE)))
+
 __device__ __forceinline__ fp ld_fp(const uint32_t* p, uint32_t n, uint32_t i, int w0) {
   fp r;
 #pragma unroll

@@ -1,7 +1,7 @@
 // A11 hash_to_G2 of every set's signing root, one lane per set.
 #include "k_common.hpp"
 
-__global__ __launch_bounds__(WAVE) void k_hash_to_g2(PipelineBuffers b, uint32_t n_sets) {
+STAGE_KERNEL void k_hash_to_g2(PipelineBuffers b, uint32_t n_sets) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets) return;
   uint8_t msg[32];

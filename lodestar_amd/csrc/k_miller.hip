@@ -12,7 +12,7 @@ __device__ __forceinline__ bool miller_set_active(const PipelineBuffers& b, uint
   return b.status[i] == BLS_OK && pk_status[i] == BLS_OK && !(b.flags[b.n + i] & SF_H_INF);
 }
 
-__global__ __launch_bounds__(WAVE) void k_miller_lines(PipelineBuffers b, uint32_t n_sets, const int8_t* pk_status) {
+STAGE_KERNEL void k_miller_lines(PipelineBuffers b, uint32_t n_sets, const int8_t* pk_status) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets || !miller_set_active(b, i, pk_status)) return;
   const g2a Q = ld_g2a(b.h_aff, b.n, i);
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(WAVE) void k_miller_lines(PipelineBuffers b, uint32
   }
 }
 
-__global__ __launch_bounds__(WAVE) void k_miller_acc(PipelineBuffers b, uint32_t n_sets, const int8_t* pk_status) {
+STAGE_KERNEL void k_miller_acc(PipelineBuffers b, uint32_t n_sets, const int8_t* pk_status) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets) return;
   fp12 f = fp12_one();

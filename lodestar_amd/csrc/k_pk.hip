@@ -47,7 +47,7 @@ __global__ __launch_bounds__(WAVE) void k_pk_aggregate(PipelineBuffers b, uint32
 // r_i * pk_i -> affine.  Bytes mode decodes the 96-byte pubkey; table mode reads k_pk_aggregate's sum.
 // pk statuses go to their own array (status[n, 2n)); the host gives them precedence over signature
 // statuses because the reference deserializes pubkeys first (worker.ts:39).
-__global__ __launch_bounds__(WAVE) void k_pk_finish(PipelineBuffers b, uint32_t n_sets, int8_t* pk_status) {
+STAGE_KERNEL void k_pk_finish(PipelineBuffers b, uint32_t n_sets, int8_t* pk_status) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets) return;
   int st = BLS_OK;

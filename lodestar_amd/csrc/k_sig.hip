@@ -2,7 +2,7 @@
 // of the random linear combination (A9), one lane per signature set.
 #include "k_common.hpp"
 
-__global__ __launch_bounds__(WAVE) void k_sig_decode(PipelineBuffers b, uint32_t n_sets) {
+STAGE_KERNEL void k_sig_decode(PipelineBuffers b, uint32_t n_sets) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets) return;
   uint8_t raw[192];
@@ -22,7 +22,7 @@ __global__ __launch_bounds__(WAVE) void k_sig_decode(PipelineBuffers b, uint32_t
   b.status[i] = (int8_t)st;
 }
 
-__global__ __launch_bounds__(WAVE) void k_sig_scale(PipelineBuffers b, uint32_t n_sets) {
+STAGE_KERNEL void k_sig_scale(PipelineBuffers b, uint32_t n_sets) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets) return;
   g2j R = jac_infinity<fp2>();

@@ -6,7 +6,7 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libblsgpu.so")
+LIB_PATH = os.environ.get("BLSGPU_LIB") or os.path.join(PKG, "libblsgpu.so")  # override: tuning variants
 
 # job / status codes (blsgpu_code)
 OK = 0
