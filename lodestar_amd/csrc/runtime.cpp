@@ -93,23 +93,19 @@ constexpr size_t kMillerLineWords = 68 * 6 * W_FP;  // MILLER_STEPS x (l0, c1, c
 struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev[kStages + 1] = {};
-  DevBuf<uint8_t> d_sigs, d_msgs, d_pkb, d_flags, d_ok, d_include;
-  DevBuf<int8_t> d_status, d_joberr;
-  DevBuf<uint32_t> d_siglen, d_pkfirst, d_pkidx, d_jobs, d_ranges, d_work, d_S, d_F, d_lines;
-  DevBuf<uint64_t> d_scalars;
-  HostBuf<uint8_t> h_sigs, h_msgs, h_pkb, h_ok;
-  HostBuf<int8_t> h_joberr;
-  HostBuf<uint32_t> h_siglen, h_pkfirst, h_pkidx, h_jobs, h_ranges;
-  HostBuf<uint64_t> h_scalars;
+  // d_in / h_in: every per-call input packed into one arena (one H2D transfer); d_res / h_res: job errors +
+  // group verdicts (one D2H transfer).  Each transfer is a blit kernel that must find a free SIMD among
+  // the full-register-file verification waves, so a batch pays for each one in queueing delay.
+  DevBuf<uint8_t> d_in, d_res, d_flags, d_ok, d_include;
+  DevBuf<int8_t> d_status;
+  DevBuf<uint32_t> d_ranges, d_work, d_S, d_F, d_lines;
+  HostBuf<uint8_t> h_in, h_res, h_ok;
+  HostBuf<uint32_t> h_ranges;
 
   void release_all() {
-    d_sigs.release(); d_msgs.release(); d_pkb.release(); d_flags.release(); d_ok.release();
-    d_include.release(); d_status.release(); d_joberr.release(); d_siglen.release(); d_pkfirst.release();
-    d_pkidx.release(); d_jobs.release(); d_ranges.release(); d_work.release(); d_S.release(); d_F.release(); d_lines.release();
-    d_scalars.release();
-    h_sigs.release(); h_msgs.release(); h_pkb.release(); h_ok.release(); h_joberr.release();
-    h_siglen.release(); h_pkfirst.release(); h_pkidx.release(); h_jobs.release(); h_ranges.release();
-    h_scalars.release();
+    d_in.release(); d_res.release(); d_flags.release(); d_ok.release(); d_include.release(); d_status.release();
+    d_ranges.release(); d_work.release(); d_S.release(); d_F.release(); d_lines.release();
+    h_in.release(); h_res.release(); h_ok.release(); h_ranges.release();
   }
 };
 
@@ -204,7 +200,6 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
   const uint32_t nj = sh.job_end - sh.job_begin;
   if (nj == 0) return BLSGPU_OK;
   HIPCHK(hipSetDevice(d.id));
-  const bool table_mode = b.pk_bytes == nullptr;
   const uint32_t s0 = sh.set_begin;
   const uint32_t stride = std::max<uint32_t>(n, 1);
   const uint32_t split_ways = (uint32_t)std::max<int64_t>(2, ctx->split_ways);
@@ -212,18 +207,31 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
   // ---- host-side job structure: groups (contiguous job ranges), scalars ------------------------
   // Non-batchable jobs are groups of their own; consecutive batchable jobs are packed until a group
   // holds >= group_sets sets.  Empty jobs get no group (rejected with EMPTY_SET).
+  // Input arena layout (256-B aligned sections; groups <= jobs bounds the ranges section):
+  //   scalars n*8 | job_first_set (nj+1)*4 | sigs n*192 | sig_len n*4 | msgs n*32 | ranges nj*8 |
+  //   table mode: set_pk_first (n+1)*4, pk_index npk*4;  bytes mode: pk_bytes n*96
+  const bool table_mode = b.pk_bytes == nullptr;
+  const uint32_t npk = table_mode ? b.set_pk_first[sh.set_end] - b.set_pk_first[s0] : 0;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_scal = 0, o_jobs = al(o_scal + (size_t)n * 8), o_sigs = al(o_jobs + (size_t)(nj + 1) * 4),
+               o_siglen = al(o_sigs + (size_t)n * 192), o_msgs = al(o_siglen + (size_t)n * 4),
+               o_ranges = al(o_msgs + (size_t)n * 32), o_pk = al(o_ranges + (size_t)nj * 8),
+               o_pkidx = al(o_pk + (size_t)(n + 1) * 4),
+               in_bytes = table_mode ? o_pkidx + (size_t)npk * 4 : o_pk + (size_t)n * 96;
+  sl.h_in.ensure(in_bytes);
+  sl.d_in.ensure(in_bytes);
+  uint8_t* const hin = sl.h_in.p;
+  uint64_t* scal = reinterpret_cast<uint64_t*>(hin + o_scal);
+  uint32_t* hjobs = reinterpret_cast<uint32_t*>(hin + o_jobs);
   std::vector<uint32_t> job_group(nj, UINT32_MAX);
   std::vector<std::pair<uint32_t, uint32_t>> group_jobs;  // [first job, end job) (shard-relative)
-  sl.h_scalars.ensure(stride);
-  uint64_t* scal = sl.h_scalars.p;
-  sl.h_jobs.ensure(nj + 1);
   {
     uint32_t cur_sets = 0;
     bool open = false;
     for (uint32_t j = 0; j < nj; j++) {
       const uint32_t gj = sh.job_begin + j;
       const uint32_t a = b.job_first_set[gj] - s0, e = b.job_first_set[gj + 1] - s0;
-      sl.h_jobs.p[j] = a;
+      hjobs[j] = a;
       const bool batchable = b.job_flags && (b.job_flags[gj] & 1u);
       if (e == a) {
         open = false;
@@ -247,56 +255,46 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
       group_jobs.back().second = j + 1;
       cur_sets += e - a;
     }
-    sl.h_jobs.p[nj] = n;
+    hjobs[nj] = n;
   }
   auto job_sets = [&](uint32_t j) {
     const uint32_t gj = sh.job_begin + j;
     return std::make_pair(b.job_first_set[gj] - s0, b.job_first_set[gj + 1] - s0);
   };
 
-  // ---- stage inputs (pinned) and copy to the device --------------------------------------------
+  // ---- stage inputs in the pinned arena and copy it to the device in one transfer ----------------
   const uint32_t sstride = b.sig_stride;
-  sl.h_sigs.ensure((size_t)stride * 192);
-  sl.h_siglen.ensure(stride);
-  sl.h_msgs.ensure((size_t)stride * 32);
+  uint8_t* hsigs = hin + o_sigs;
+  uint32_t* hsiglen = reinterpret_cast<uint32_t*>(hin + o_siglen);
   for (uint32_t i = 0; i < n; i++) {
     uint32_t len = b.sig_len[s0 + i];
     uint32_t cl = (len == 96 || len == 192) ? len : 0;
-    memcpy(sl.h_sigs.p + (size_t)i * 192, b.sigs + (size_t)(s0 + i) * sstride, cl);
-    sl.h_siglen.p[i] = len;
+    memcpy(hsigs + (size_t)i * 192, b.sigs + (size_t)(s0 + i) * sstride, cl);
+    hsiglen[i] = len;
   }
-  memcpy(sl.h_msgs.p, b.msgs + (size_t)s0 * 32, (size_t)n * 32);
-  uint32_t npk = 0;
+  memcpy(hin + o_msgs, b.msgs + (size_t)s0 * 32, (size_t)n * 32);
   if (table_mode) {
-    sl.h_pkfirst.ensure(stride + 1);
-    uint32_t base = b.set_pk_first[s0];
-    npk = b.set_pk_first[sh.set_end] - base;
-    for (uint32_t i = 0; i <= n; i++) sl.h_pkfirst.p[i] = b.set_pk_first[s0 + i] - base;
-    sl.h_pkidx.ensure(std::max<uint32_t>(npk, 1));
-    memcpy(sl.h_pkidx.p, b.pk_index + base, (size_t)npk * 4);
+    uint32_t* hpkfirst = reinterpret_cast<uint32_t*>(hin + o_pk);
+    const uint32_t base = b.set_pk_first[s0];
+    for (uint32_t i = 0; i <= n; i++) hpkfirst[i] = b.set_pk_first[s0 + i] - base;
+    memcpy(hin + o_pkidx, b.pk_index + base, (size_t)npk * 4);
   } else {
-    sl.h_pkb.ensure((size_t)stride * 96);
-    memcpy(sl.h_pkb.p, b.pk_bytes + (size_t)s0 * 96, (size_t)n * 96);
+    memcpy(hin + o_pk, b.pk_bytes + (size_t)s0 * 96, (size_t)n * 96);
   }
   const uint32_t ng0 = (uint32_t)group_jobs.size();
   const uint32_t max_ranges = std::max<uint32_t>(std::max(ng0, nj), 1);
-  sl.h_ranges.ensure(2 * max_ranges);
+  uint32_t* hranges = reinterpret_cast<uint32_t*>(hin + o_ranges);
   for (uint32_t g = 0; g < ng0; g++) {
-    sl.h_ranges.p[2 * g] = job_sets(group_jobs[g].first).first;
-    sl.h_ranges.p[2 * g + 1] = job_sets(group_jobs[g].second - 1).second;
+    hranges[2 * g] = job_sets(group_jobs[g].first).first;
+    hranges[2 * g + 1] = job_sets(group_jobs[g].second - 1).second;
   }
 
-  sl.d_sigs.ensure((size_t)stride * 192);
-  sl.d_siglen.ensure(stride);
-  sl.d_msgs.ensure((size_t)stride * 32);
-  sl.d_scalars.ensure(stride);
   sl.d_flags.ensure((size_t)stride * 2);
   sl.d_status.ensure((size_t)stride * 2);
   sl.d_include.ensure(stride);
-  sl.d_jobs.ensure(nj + 1);
-  sl.d_joberr.ensure(nj);
-  sl.d_ranges.ensure(2 * max_ranges);
-  sl.d_ok.ensure(max_ranges);
+  const size_t o_ok = al(nj), res_bytes = o_ok + max_ranges;
+  sl.d_res.ensure(res_bytes);
+  sl.h_res.ensure(res_bytes);
   sl.d_S.ensure((size_t)W_G2J * max_ranges);
   sl.d_F.ensure((size_t)W_FP12 * max_ranges);
   // work area: sig_aff, h_aff, pk_jac, pk_aff, rsig, f
@@ -304,35 +302,23 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
   sl.d_work.ensure(work_words);
   sl.d_lines.ensure((size_t)stride * kMillerLineWords);
   hipStream_t s = sl.stream;
-  HIPCHK(hipMemcpyAsync(sl.d_sigs.p, sl.h_sigs.p, (size_t)n * 192, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(sl.d_siglen.p, sl.h_siglen.p, (size_t)n * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(sl.d_msgs.p, sl.h_msgs.p, (size_t)n * 32, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(sl.d_scalars.p, sl.h_scalars.p, (size_t)n * 8, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(sl.d_jobs.p, sl.h_jobs.p, (size_t)(nj + 1) * 4, hipMemcpyHostToDevice, s));
-  if (ng0) HIPCHK(hipMemcpyAsync(sl.d_ranges.p, sl.h_ranges.p, (size_t)ng0 * 8, hipMemcpyHostToDevice, s));
-  if (table_mode) {
-    sl.d_pkfirst.ensure(stride + 1);
-    sl.d_pkidx.ensure(std::max<uint32_t>(npk, 1));
-    HIPCHK(hipMemcpyAsync(sl.d_pkfirst.p, sl.h_pkfirst.p, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, s));
-    if (npk) HIPCHK(hipMemcpyAsync(sl.d_pkidx.p, sl.h_pkidx.p, (size_t)npk * 4, hipMemcpyHostToDevice, s));
-  } else {
-    sl.d_pkb.ensure((size_t)stride * 96);
-    HIPCHK(hipMemcpyAsync(sl.d_pkb.p, sl.h_pkb.p, (size_t)n * 96, hipMemcpyHostToDevice, s));
-  }
+  uint8_t* const din = sl.d_in.p;
+  HIPCHK(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, s));
+  uint8_t* const d_ok0 = sl.d_res.p + o_ok;
 
   PipelineBuffers pb;
   pb.n = stride;
-  pb.sigs = sl.d_sigs.p;
-  pb.sig_len = sl.d_siglen.p;
+  pb.sigs = din + o_sigs;
+  pb.sig_len = reinterpret_cast<uint32_t*>(din + o_siglen);
   pb.sig_stride = 192;
-  pb.msgs = sl.d_msgs.p;
-  pb.pk_bytes = table_mode ? nullptr : sl.d_pkb.p;
-  pb.set_pk_first = table_mode ? sl.d_pkfirst.p : nullptr;
-  pb.pk_index = table_mode ? sl.d_pkidx.p : nullptr;
+  pb.msgs = din + o_msgs;
+  pb.pk_bytes = table_mode ? nullptr : din + o_pk;
+  pb.set_pk_first = table_mode ? reinterpret_cast<uint32_t*>(din + o_pk) : nullptr;
+  pb.pk_index = table_mode ? reinterpret_cast<uint32_t*>(din + o_pkidx) : nullptr;
   pb.pk_table = d.table.p;
   pb.pk_table_n = d.table_n;
-  pb.scalars = sl.d_scalars.p;
-  pb.job_first_set = sl.d_jobs.p;
+  pb.scalars = reinterpret_cast<uint64_t*>(din + o_scal);
+  pb.job_first_set = reinterpret_cast<uint32_t*>(din + o_jobs);
   pb.n_jobs = nj;
   uint32_t* w = sl.d_work.p;
   pb.sig_aff = w; w += (size_t)stride * W_G2A;
@@ -344,7 +330,7 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
   pb.lines = sl.d_lines.p;
   pb.flags = sl.d_flags.p;
   pb.status = sl.d_status.p;
-  pb.job_err = sl.d_joberr.p;
+  pb.job_err = reinterpret_cast<int8_t*>(sl.d_res.p);
   pb.include = sl.d_include.p;
 
   // ---- kernel pipeline ---------------------------------------------------------------------------
@@ -366,15 +352,12 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
   launch_miller_sets(pb, n, s);
   launch_job_mask(pb, s);
   mark(6);
-  launch_group_reduce(pb, sl.d_ranges.p, ng0, sl.d_S.p, sl.d_F.p, s);
+  launch_group_reduce(pb, reinterpret_cast<uint32_t*>(din + o_ranges), ng0, sl.d_S.p, sl.d_F.p, s);
   mark(7);
-  launch_group_check(sl.d_S.p, sl.d_F.p, ng0, sl.d_ok.p, s);
+  launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, s);
   mark(8);
   HIPCHK(hipGetLastError());
-  sl.h_joberr.ensure(nj);
-  sl.h_ok.ensure(max_ranges);
-  HIPCHK(hipMemcpyAsync(sl.h_joberr.p, sl.d_joberr.p, nj, hipMemcpyDeviceToHost, s));
-  if (ng0) HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, ng0, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(sl.h_res.p, sl.d_res.p, o_ok + ng0, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   st.groups += ng0;
   if (prof) {
@@ -388,7 +371,7 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
   // ---- per-job results ---------------------------------------------------------------------------
   std::vector<int> jr(nj, 0);
   for (uint32_t j = 0; j < nj; j++) {
-    const int err = sl.h_joberr.p[j];
+    const int err = (int8_t)sl.h_res.p[j];
     jr[j] = err ? -err : 2;  // 2 = pending
   }
   // pending work: lists of clean jobs whose batch equation failed
@@ -398,7 +381,7 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
     for (uint32_t j = group_jobs[g].first; j < group_jobs[g].second; j++)
       if (jr[j] == 2) clean.push_back(j);
     if (clean.empty()) continue;
-    if (sl.h_ok.p[g]) {
+    if (sl.h_res.p[o_ok + g]) {
       for (uint32_t j : clean) jr[j] = 1;
       if (group_jobs[g].second - group_jobs[g].first > 1)
         for (uint32_t j : clean) st.batch_sigs_success += job_sets(j).second - job_sets(j).first;
