@@ -468,10 +468,17 @@ extern "C" {
 int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
   if (!out) return BLSGPU_ERR_ARGS;
   *out = nullptr;
-  // Every slot needs its own hardware queue: kernels of streams that share one run in order, and a
-  // batch's single-wave tail (k_group_check) would then block the next batch's stage kernels.  HIP reads
-  // this once, at its initialization; an explicit setting by the user wins.
-  setenv("GPU_MAX_HW_QUEUES", "16", 0);
+  // Slots need hardware queues of their own: kernels of streams that share one run in order, so a batch's
+  // long single-batch tail (k_group_check) blocks the next batch's stage kernels.  HIP's default (and the
+  // usual environment) is 4 queues per process; on MI355X 8 measured 1.70M vs 1.32M sets/s on C2 with 12
+  // slots, and 16 fails queue creation (HSA_STATUS_ERROR_OUT_OF_RESOURCES) -- profiles/r01_hwq.json.  So a
+  // setting below 8 is raised to 8 (BLSGPU_KEEP_HW_QUEUES=1 keeps it).  HIP reads it once, at its
+  // initialization, so this only takes effect when blsgpu_init is the process's first HIP call.
+  {
+    const char* q = getenv("GPU_MAX_HW_QUEUES");
+    const char* keep = getenv("BLSGPU_KEEP_HW_QUEUES");
+    if (!(keep && keep[0] == '1') && (!q || atoi(q) < 8)) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+  }
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return BLSGPU_ERR_NO_DEVICE;
   std::vector<int> ids;
