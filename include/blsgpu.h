@@ -83,7 +83,10 @@ typedef struct blsgpu_stats {
   double stage_ms[8];
 } blsgpu_stats;
 
-/* Create a context on the given HIP devices (NULL / n <= 0: every visible device). */
+/* Create a context on the given HIP devices (NULL / n <= 0: every visible device).
+ * When this is the process's first HIP call it raises GPU_MAX_HW_QUEUES below 8 to 8, so concurrent calls
+ * (one runtime slot and stream each) do not share in-order hardware queues; BLSGPU_KEEP_HW_QUEUES=1 keeps
+ * the caller's setting. */
 int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out);
 /* Waits for in-flight submissions, fails queued ones with BLSGPU_ERR_CLOSED, frees everything. */
 void blsgpu_destroy(blsgpu_ctx* ctx);
