@@ -254,10 +254,13 @@ def pmc_traffic(kernel, n_sets):
     if n_sets != PMC_SETS_PER_LAUNCH or not os.path.exists(PMC_FILE):
         return None
     with open(PMC_FILE) as fh:
-        k = json.load(fh)["kernels"].get(kernel)
-    if not k:
+        table = json.load(fh)["kernels"]
+    # the Miller stage is two launches per batch (k_miller.hip): line pass + accumulation pass
+    parts = {"k_miller_sets": ["k_miller_lines", "k_miller_acc"]}.get(kernel, [kernel])
+    if not all(p in table for p in parts):
         return None
-    return round(2 * 1024 * k["FETCH_SIZE_kB_per_launch"] + 1024 * k["WRITE_SIZE_kB_per_launch"])
+    return round(sum(2 * 1024 * table[p]["FETCH_SIZE_kB_per_launch"] + 1024 * table[p]["WRITE_SIZE_kB_per_launch"]
+                     for p in parts))
 
 
 def _cpu_worker(job):

@@ -1,0 +1,47 @@
+"""Folds the two rocprofv3 PMC passes of tools/gpurun/pmc.sh (FETCH_SIZE, WRITE_SIZE; csv output) into
+profiles/<tag>_pmc_traffic.json: per kernel, the counter summed over each dispatch's rows and averaged over
+dispatches (kB per launch, as rocprofv3 reports them).  bench.py turns them into HBM bytes per launch.
+
+    python tools/pmc_to_json.py gpurun_out/r01_pmc2 profiles/r01_pmc_traffic.json
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def per_launch(path, counter):
+    per_dispatch = defaultdict(float)
+    names = {}
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            if row["Counter_Name"] != counter:
+                continue
+            per_dispatch[row["Dispatch_Id"]] += float(row["Counter_Value"])
+            names[row["Dispatch_Id"]] = row["Kernel_Name"].split("(")[0]
+    acc = defaultdict(list)
+    for d, v in per_dispatch.items():
+        acc[names[d]].append(v)
+    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
+
+
+def main(prefix, out):
+    f = per_launch(f"{prefix}_pmc_FETCH_SIZE/run_counter_collection.csv", "FETCH_SIZE")
+    w = per_launch(f"{prefix}_pmc_WRITE_SIZE/run_counter_collection.csv", "WRITE_SIZE")
+    kernels = {k: {"FETCH_SIZE_kB_per_launch": round(f.get(k, (0, 0))[0], 1),
+                   "WRITE_SIZE_kB_per_launch": round(w.get(k, (0, 0))[0], 1),
+                   "launches": f.get(k, (0, 0))[1]} for k in sorted(set(f) | set(w))}
+    doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, kernel trace only), "
+                     "bench.py --steps 2 --warmup 1 --inflight 1 --no-profile (C2, 16384 sets per launch)",
+           "units": "kB per launch as reported; gfx950 FETCH_SIZE counts 1/2 of wide streaming reads "
+                    "(MI355X_MICROARCH.md HBM section) -> bytes = 2 x 1024 x FETCH_SIZE; WRITE_SIZE exact",
+           "kernels": kernels}
+    with open(out, "w") as fh:
+        json.dump(doc, fh, indent=1)
+    return doc
+
+
+if __name__ == "__main__":
+    d = main(sys.argv[1], sys.argv[2])
+    for k, v in d["kernels"].items():
+        print(k, v)
