@@ -1,0 +1,67 @@
+/* blscpu.h -- TEST INFRASTRUCTURE ONLY: the C restatement of the verification path (CPU oracle and the
+ * bench's cpu_baseline).  Only tests/, __graft_entry__ and bench.py's cpu_baseline leg load
+ * oracle/libblscpu.so; the product (lodestar_amd/libblsgpu.so) never links or calls it.
+ *
+ * It restates, on 6 x 64-bit Montgomery limbs (unsigned __int128 products), the arithmetic that the
+ * reference delegates to @chainsafe/bls@7.1.1 -> @chainsafe/blst@0.2.4 (reference yarn.lock:436-451, not
+ * vendored), following the same specifications as oracle/bls12_381.py, and the reference's pool policy:
+ *   blscpu_verify_jobs  <- BlsMultiThreadWorkerPool.verifySignatureSets + prepareWork + worker
+ *                          verifyManySignatureSets (packages/beacon-node/src/chain/bls/multithread/
+ *                          index.ts:134-174,386-401; worker.ts:32-108; maybeBatch.ts:16-39)
+ *   blscpu_aggregate_pubkeys <- PublicKey.aggregate(pks).toBytes() (chain/bls/utils.ts:5-16)
+ *   blscpu_key_validate <- PublicKey.fromBytes(pk, validate=true) (state-transition/src/block/
+ *                          processDeposit.ts:56-64)
+ * Job results use the codes of include/blsgpu.h (1 valid, 0 invalid, -code rejected).
+ */
+#ifndef BLSCPU_H
+#define BLSCPU_H
+#include <stdint.h>
+
+#include "../include/blsgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct blscpu_table blscpu_table;
+
+/* decoded trusted pubkey table (96-byte uncompressed affine entries); NULL on a malformed entry
+ * (*bad_index receives its index) */
+blscpu_table* blscpu_table_create(const uint8_t* pk96, uint32_t n, uint32_t* bad_index);
+void blscpu_table_free(blscpu_table* t);
+
+/* Element-wise helpers (n items, n_threads worker threads; 0 = all cores).  Return 0 or a status. */
+int blscpu_sk_to_pk(uint32_t n, const uint8_t* sk32_be, uint8_t* pk96_out, int n_threads);
+int blscpu_sign(uint32_t n, const uint8_t* sk32_be, const uint8_t* msg32, uint8_t* sig96_out, int n_threads);
+int blscpu_hash_to_g2(uint32_t n, const uint8_t* msg32, uint8_t* g2_192_out, int n_threads);
+/* Signature.fromBytes(validate = true) status of one signature */
+int blscpu_sig_status(const uint8_t* sig, uint32_t len);
+/* n sets of a batch's pubkey fields -> uncompressed (out_len 96) or compressed (48) aggregates; status[i] */
+int blscpu_aggregate_pubkeys(const blsgpu_batch* b, const blscpu_table* table, uint8_t* out, uint32_t out_len,
+                             int8_t* status, int n_threads);
+/* KeyValidate of an untrusted 48-byte compressed or 96-byte uncompressed pubkey: 0 ok or a code
+ * (BAD_ENCODING, POINT_NOT_ON_CURVE, POINT_NOT_IN_GROUP, PK_IS_INFINITY, INVALID_SIZE) */
+int blscpu_key_validate(const uint8_t* pk, uint32_t len);
+/* decode an untrusted compressed/uncompressed pubkey (no subgroup check) to 96-byte uncompressed */
+int blscpu_pk_decode(const uint8_t* pk, uint32_t len, uint8_t* pk96_out);
+
+typedef struct blscpu_stats {
+  uint32_t work_requests;      /* worker dispatches (prepareWork packages) */
+  uint32_t batch_retries;      /* failed batch chunks re-verified per job (blsThreadPool.batchRetries) */
+  uint32_t batch_sigs_success; /* sets accepted by a batch chunk (blsThreadPool.batchSigsSuccess) */
+  uint32_t threads;
+} blscpu_stats;
+
+/* The reference pool over one blsgpu_batch (every mode of include/blsgpu.h; table mode needs `table`).
+ * job_result[n_jobs] as blsgpu_verify.  Results do not depend on `seed` or the thread count. */
+int blscpu_verify_jobs(const blsgpu_batch* b, const blscpu_table* table, int8_t* job_result, int n_threads,
+                       blscpu_stats* stats);
+
+/* instrumentation: Fp multiplications (mul + sqr) executed by the calling thread since the last reset */
+void blscpu_count_reset(void);
+uint64_t blscpu_count_get(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
