@@ -53,10 +53,11 @@ def gen_sigs(ctx, sk_bytes_list, msgs):
     return sigs
 
 
-def build_workload(ctx, config, rank, world=1):
-    """Returns dict of numpy inputs for verify_raw + description."""
+def build_workload(ctx, config, rank, world=1, n_dev=1):
+    """Returns dict of numpy inputs for verify_raw + description.  n_dev > 1: one call spans n_dev in-process
+    devices (the runtime shards it), so C2 carries 16,384 sets per device."""
     if config == "C2":
-        n = 16384
+        n = 16384 * n_dev
         sks, pks = gen_keys(ctx, n)
         ctx.upload_pubkeys(0, pks)
         msgs = [msg_j(rank * n + j) for j in range(n)]
@@ -64,9 +65,9 @@ def build_workload(ctx, config, rank, world=1):
         w = dict(job_first_set=np.arange(n + 1, dtype=np.uint32), sigs=np.frombuffer(sigs, np.uint8),
                  sig_len=np.full(n, 96, np.uint32), msgs=np.frombuffer(b"".join(msgs), np.uint8),
                  set_pk_first=np.arange(n + 1, dtype=np.uint32), pk_index=np.arange(n, dtype=np.uint32),
-                 job_flags=np.ones(n, np.uint8), sig_stride=96)
+                 job_flags=np.ones(n, np.uint8), sig_stride=96, pks_table=pks)
         desc = {"workload": "C2 gossip attestation flood: 16384 single-pubkey sets per GPU, 1 set per batchable job",
-                "sets_per_step_per_gpu": n, "pubkeys_per_set": 1, "pk_mode": "device table",
+                "sets_per_step_per_gpu": n // n_dev, "pubkeys_per_set": 1, "pk_mode": "device table",
                 "sig_encoding": "compressed 96 B", "distinct_messages": n}
         return w, n, desc, 1
     if config == "C3":
@@ -263,42 +264,38 @@ def pmc_traffic(kernel, n_sets):
                      for p in parts))
 
 
-def _cpu_worker(job):
-    """One baseline worker (a spawned process: no GPU state): derives its sets untimed, then times
-    verifySignatureSetsMaybeBatch over its chunks of 16 sets."""
-    first, msgs, sigs, chunk = job
-    from oracle import bls12_381 as bls
+BLST_SETS_PER_CORE = 2200.0  # published anchor: ~0.9 ms/set/thread, x2 batched
 
-    n = len(msgs) // 32
-    sets = [(bls.sk_to_pk(interop_sk(first + i)), msgs[32 * i : 32 * i + 32], sigs[96 * i : 96 * i + 96])
-            for i in range(n)]
-    bls.verify_signature_sets_maybe_batch(sets[:1])  # untimed warm-up (lazy oracle constants)
+
+def cpu_baseline(work, expected, max_threads=16):
+    """The reference pool restated in C (oracle/blscpu.c: 6 x 64-bit Montgomery, the pool's job split, >= 16-job
+    batch chunks and per-job fallback; kind "port") on this host's cores, on the SAME step the GPU times (all of
+    its sets, same inputs), with the result checked against the GPU's.  The blst pool itself cannot run here
+    (not vendored, no network): its published per-core anchor is reported beside."""
+    from oracle import cpu
+
+    threads = max(1, min(max_threads, os.cpu_count() or 1))  # the GPU box's CPU share is 16 threads
+    call = {k: v for k, v in work.items() if k != "expected"}
+    table = cpu.Table(work["pks_table"]) if "pks_table" in work else None
+    call.pop("pks_table", None)
     t0 = time.perf_counter()
-    ok = True
-    for c in range(0, n, chunk):
-        ok &= bls.verify_signature_sets_maybe_batch(sets[c : c + chunk], rng=bls.SplitMix64(SEED + first + c))
-    return time.perf_counter() - t0, ok
-
-
-def cpu_baseline(work, n_sample=2048, chunk=16, workers=8):
-    """Oracle ('port') timed on this host's cores, shaped like the reference worker pool: `workers`
-    processes (BlsMultiThreadWorkerPool, multithread/index.ts:134-174), each verifying chunks of 16 sets
-    (BATCHABLE_MIN_PER_CHUNK, worker.ts:17) with pure-Python big ints.  value = sample / slowest worker."""
-    import multiprocessing as mp
-
-    workers = max(1, min(workers, os.cpu_count() or 1))
-    per = n_sample // workers
-    jobs = [(w * per, bytes(work["msgs"][32 * w * per : 32 * (w + 1) * per]),
-             bytes(work["sigs"][96 * w * per : 96 * (w + 1) * per]), chunk) for w in range(workers)]
-    with mp.get_context("spawn").Pool(workers) as pool:  # fresh interpreters, never a fork of the GPU process
-        res = pool.map(_cpu_worker, jobs)
-    dt = max(r[0] for r in res)
-    assert all(r[1] for r in res), "oracle rejected the GPU-generated workload"
-    n = per * workers
-    return {"value": round(n / dt, 3), "unit": "sets/s", "cores": workers, "kind": "port",
-            "sample": f"{n} C2 sets, {workers} worker processes x {per} sets in batches of {chunk}, pure-Python "
-                      f"oracle (oracle/bls12_381.py), slowest worker {dt:.1f} s; reference blst pool unavailable "
-                      f"offline"}
+    res, st = cpu.verify_jobs(table=table, threads=threads, **call)
+    dt = time.perf_counter() - t0
+    assert np.array_equal(res, expected), "C oracle and GPU disagree on the bench step"
+    n = len(call["sig_len"])
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((l.split(":", 1)[1].strip() for l in fh if l.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"value": round(n / dt, 2), "unit": "sets/s", "cores": threads, "kind": "port",
+            "sample": f"the full bench step ({n} sets, {st.work_requests} worker requests of >= 128 sets, "
+                      f"batch chunks of >= 16 jobs) through oracle/blscpu.c on {threads} threads of '{model}' "
+                      f"(os.cpu_count() {os.cpu_count()}), {dt:.2f} s, results identical to the GPU's",
+            "blst_anchor_sets_per_s": BLST_SETS_PER_CORE * threads,
+            "blst_anchor": f"{BLST_SETS_PER_CORE:.0f} sets/s/core (reference lodestar.ts:454 ~0.9 ms/set/thread, "
+                           f"x2 batched index.ts:44) x {threads} cores; the blst pool is not runnable offline"}
 
 
 def main():
@@ -314,6 +311,9 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
 
+    # Concurrent calls use one runtime slot (HIP stream) each; HIP reads GPU_MAX_HW_QUEUES once, at its first
+    # call, so the launcher sets it (the box default of 4 makes 12 slot streams share 4 in-order queues).
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -328,12 +328,19 @@ def main():
 
     from lodestar_amd.native import Context
 
-    ctx = Context([local_rank])
+    # one process per GPU under torch.distributed.run; without a launcher, --gpus N uses N devices in-process
+    # (each call sharded over them by the runtime)
+    n_dev = args.gpus if world == 1 else 1
+    if n_dev > 1 and args.config != "C2":
+        raise SystemExit("in-process multi-GPU runs take --config C2 (launch other configs per rank)")
+    devices = list(range(n_dev)) if world == 1 else [local_rank]
+    ctx = Context(devices)
     ctx.set_option("group_sets", args.group_sets)
     ctx.set_option("slots", max(1, args.inflight))
-    work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world)
+    work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev)
     call = dict(work)
     expected = call.pop("expected", None)
+    call.pop("pks_table", None)
     if expected is None:
         expected = np.ones(len(call["job_first_set"]) - 1, np.int8)
 
@@ -373,6 +380,7 @@ def main():
     dt = max_over_ranks(dt, dist)
     strong = desc.pop("scaling", "weak") == "strong"
     total_sets = (desc["total_sets_per_step"] if strong else n_sets * world) * args.steps
+    n_gpus = world * n_dev
     value = total_sets / dt
     # ---- isolated batches (untimed): p50 latency of one call, and per-stage kernel times ----
     lat = []
@@ -384,7 +392,7 @@ def main():
         "metric": "verified signature sets/sec (node)",
         "value": round(value, 2),
         "unit": "sets/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(dt * 1e3 / args.steps, 3),
@@ -394,7 +402,7 @@ def main():
         "dtype": "u32/u64 (28-bit-limb Montgomery integer arithmetic)",
         "data": "synthetic (interop keys, SHA-256 messages, signatures generated on the GPU before timing)",
         "config": dict(desc, group_sets=args.group_sets, batch_groups_per_step=groups, inflight=args.inflight,
-                       parallelism=f"shard-by-set x{world}, no collective"),
+                       parallelism=f"shard-by-job x{n_gpus} ({'one process per GPU' if world > 1 else 'in-process devices'}), no collective"),
         "p50_batch_latency_ms": round(float(np.median(lat)), 3),
     }
     if not args.no_profile:
@@ -403,9 +411,10 @@ def main():
         for _ in range(2):
             stage_acc += np.array(step().stage_ms[:8])
         ctx.set_option("profile", 0)
-        out["roofline"] = roofline(stage_acc / 2, n_sets, groups, pk_per_set, value / world)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(work)
+        out["roofline"] = roofline(stage_acc / 2, n_sets // n_dev, groups // n_dev, pk_per_set, value / n_gpus)
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(dict(call, pks_table=work["pks_table"]) if "pks_table" in work else call,
+                                           expected)
     if rank == 0:
         print(json.dumps(out), flush=True)
     pool.shutdown()

@@ -12,6 +12,14 @@
  *   blsgpu_pubkeys_upload           <- the pubkey cache the sets draw from (state-transition
  *                                      src/cache/pubkeyCache.ts:56-77, epochContext.ts:702-705)
  *   blsgpu_destroy                  <- IBlsVerifier.close (chain/bls/interface.ts:45)
+ *   blsgpu_aggregate_pubkeys        <- PublicKey.aggregate(pks).toBytes() (chain/bls/utils.ts:5-16,
+ *                                      multithread/index.ts:160)
+ *   blsgpu_key_validate             <- PublicKey.fromBytes(pk, CoordType.affine, validate = true) for untrusted
+ *                                      keys (state-transition/src/block/processDeposit.ts:56-64,
+ *                                      beacon-node/test/spec/general/bls.ts:33-42)
+ *   blsgpu_signing_roots            <- computeSigningRoot (state-transition/src/util/signingRoot.ts:7-13)
+ *   blsgpu_shard_jobs               <- the job sharding rule the runtime applies over devices (also restated
+ *                                      by lodestar_amd/shard.py for one-process-per-GPU launches)
  *
  * Conventions: plain pointers and sizes, caller-owned buffers, every call copies its inputs before
  * returning (blsgpu_submit included), `int` status (0 = ok).  Per-job results use the blst error names
@@ -28,7 +36,7 @@
 extern "C" {
 #endif
 
-#define BLSGPU_ABI_VERSION 1
+#define BLSGPU_ABI_VERSION 2
 
 enum blsgpu_code {
   BLSGPU_OK = 0,
@@ -58,9 +66,17 @@ typedef struct blsgpu_batch {
   uint32_t n_jobs;
   const uint32_t* job_first_set; /* [n_jobs + 1], non-decreasing, job_first_set[n_jobs] == n_sets */
   const uint8_t* job_flags;      /* [n_jobs] bit0 = batchable (VerifySignatureOpts.batchable); NULL = none */
-  /* Public keys, one of two modes:
-   *  bytes mode: pk_bytes[96 * i] = set i's (already aggregated) pubkey, uncompressed affine (ZCash);
-   *  table mode: set i aggregates table entries pk_index[set_pk_first[i] .. set_pk_first[i+1]). */
+  /* Public keys, one of three modes (set_pk_first is [n_sets + 1], non-decreasing, starting at 0):
+   *  bytes mode (pk_bytes, set_pk_first == NULL): pk_bytes[96 * i] = set i's pubkey, uncompressed affine
+   *    (ZCash) -- what the pool sends today, getAggregatedPubkey(set).toBytes() (multithread/index.ts:160);
+   *  bytes-aggregate mode (pk_bytes and set_pk_first): set i aggregates the keys pk_bytes[96 * k],
+   *    k in [set_pk_first[i], set_pk_first[i+1]) -- the aggregate ISignatureSet of any PublicKey objects
+   *    (pk.toBytes()), aggregated on the GPU; a set with no keys rejects with EMPTY_AGGREGATE_ARRAY;
+   *  table mode (pk_bytes == NULL): set i aggregates device-table entries pk_index[set_pk_first[i] ..
+   *    set_pk_first[i+1]) (blsgpu_pubkeys_upload); an index beyond the table fails the call with ERR_ARGS.
+   * Keys are trusted (subgroup-checked when they entered the pubkey cache); malformed bytes reject the job
+   * with BLST_BAD_ENCODING / BLST_POINT_NOT_ON_CURVE, an aggregate equal to the identity with
+   * BLST_PK_IS_INFINITY. */
   const uint8_t* pk_bytes;
   const uint32_t* set_pk_first; /* [n_sets + 1] */
   const uint32_t* pk_index;
@@ -70,23 +86,28 @@ typedef struct blsgpu_batch {
   uint32_t sig_stride;
   uint64_t seed; /* random-linear-combination scalars: fixed seed for comparison runs, 0 = OS CSPRNG */
 } blsgpu_batch;
+/* Identical signing roots within a call are hashed to G2 once, and within a batch group the sets that sign
+ * the same root are paired once, against sum_i r_i pk_i (option "dedupe", default 1). */
 
 typedef struct blsgpu_stats {
   uint32_t groups;             /* batch groups checked (one final exponentiation each) */
   uint32_t batch_retries;      /* failed groups re-checked per job (metric blsThreadPool.batchRetries) */
   uint32_t batch_sigs_success; /* sets accepted by a batch group (metric blsThreadPool.batchSigsSuccess) */
   uint32_t devices_used;
-  double device_ms; /* wall time of the device phase (max over devices) */
+  double device_ms; /* wall time of the call from dispatch to completion */
   /* With option "profile" = 1: per-stage kernel time (HIP events on the launch stream, device 0 shard):
    * 0 sig_decode 1 hash_to_g2 2 pk_aggregate 3 pk_finish 4 sig_scale 5 miller_sets
    * 6 group_sig_miller 7 group_finish */
   double stage_ms[8];
+  uint32_t unique_messages; /* distinct signing roots hashed to G2 */
+  uint32_t pairing_units;   /* Miller loops of the batch pass (sets, or same-message units) */
 } blsgpu_stats;
 
-/* Create a context on the given HIP devices (NULL / n <= 0: every visible device).
- * When this is the process's first HIP call it raises GPU_MAX_HW_QUEUES below 8 to 8, so concurrent calls
- * (one runtime slot and stream each) do not share in-order hardware queues; BLSGPU_KEEP_HW_QUEUES=1 keeps
- * the caller's setting. */
+/* Create a context on the given HIP devices (NULL / n <= 0: every visible device).  Each device gets 4
+ * runtime slots (option "slots"), each a HIP stream served by one long-lived dispatcher thread; concurrent
+ * calls run on different slots.  Streams sharing an in-order hardware queue serialize, so the launcher
+ * should set GPU_MAX_HW_QUEUES >= slots before the process's first HIP call (the library does not touch
+ * the environment). */
 int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out);
 /* Waits for in-flight submissions, fails queued ones with BLSGPU_ERR_CLOSED, frees everything. */
 void blsgpu_destroy(blsgpu_ctx* ctx);
@@ -94,22 +115,56 @@ int blsgpu_device_count(const blsgpu_ctx* ctx);
 
 /* Trusted pubkey table (replicated on every device): entries [first_index, first_index + n) from
  * 96-byte uncompressed affine encodings.  Returns BLSGPU_BAD_ENCODING / _POINT_NOT_ON_CURVE for a
- * malformed entry (nothing is written in that case). */
+ * malformed entry (nothing is written on that device in that case), BLSGPU_ERR_ARGS when first_index is
+ * beyond the current table size (no gaps).  Devices are updated one after the other; a call that uses the
+ * new indices before the upload returns may fail with BLSGPU_ERR_ARGS, never verify against stale keys. */
 int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* pk96, uint32_t n);
 uint32_t blsgpu_pubkeys_count(const blsgpu_ctx* ctx);
 
 /* Synchronous verification.  job_result[n_jobs]: 1 valid / 0 invalid / -code.  Returns a call-level
- * status (BLSGPU_OK even when some jobs are invalid or rejected). */
+ * status (BLSGPU_OK even when some jobs are invalid or rejected; a HIP failure rejects the jobs of the
+ * affected shard with -BLSGPU_DEVICE_ERROR). */
 int blsgpu_verify(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result, blsgpu_stats* stats);
 
 /* Asynchronous verification: inputs are copied before return; `done(user, status)` runs on a runtime
- * thread once job_result / stats are written.  For the N-API addon's threadsafe-function bridge. */
+ * dispatcher thread once job_result / stats are written (status BLSGPU_ERR_CLOSED when the context was
+ * destroyed before the call ran).  For the N-API addon's threadsafe-function bridge. */
 typedef void (*blsgpu_done_cb)(void* user, int status);
 int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result, blsgpu_stats* stats,
                   blsgpu_done_cb done, void* user);
 
-/* Tunables: "group_sets" (target sets per batch group, default 64), "max_devices", "profile" (0/1). */
+/* Tunables: "group_sets" (sets per batch group before a new one opens, default 256), "slots" (runtime slots
+ * per device, only grows, default 4), "max_devices" (devices one call may shard over, default all),
+ * "dedupe" (message dedupe + same-message pairing, 0/1, default 1), "profile" (per-stage kernel times in
+ * blsgpu_stats.stage_ms, 0/1).  Applies to calls submitted afterwards. */
 int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value);
+
+/* PublicKey.aggregate(set pubkeys).toBytes() for every set of `b` (only n_sets and the pubkey fields are
+ * read; any of the three modes): out[out_len * i], out_len 96 (uncompressed) or 48 (compressed);
+ * status[i] = 0, EMPTY_AGGREGATE (no keys) or the first malformed key's code.  An aggregate equal to the
+ * identity is encoded as the identity. */
+int blsgpu_aggregate_pubkeys(blsgpu_ctx* ctx, const blsgpu_batch* b, uint8_t* out, uint32_t out_len,
+                             int8_t* status);
+
+/* KeyValidate of n untrusted pubkeys (pks[stride * i], pk_len 48 compressed or 96 uncompressed): status[i]
+ * = 0 or BAD_ENCODING / POINT_NOT_ON_CURVE / PK_IS_INFINITY / POINT_NOT_IN_GROUP; out96 (nullable)
+ * receives the uncompressed encoding of every valid key (bytes-mode input of blsgpu_verify). */
+int blsgpu_key_validate(blsgpu_ctx* ctx, uint32_t n, const uint8_t* pks, uint32_t pk_len, uint32_t stride,
+                        uint8_t* out96, int8_t* status);
+
+/* Signing roots: out32[32 i] = hash_tree_root(SigningData{object_root_i, domain_i}) where object_root_i is
+ * objects[object_stride * i] itself (BLSGPU_ROOT_OBJECT, 32 B) or hash_tree_root of the SSZ-serialized
+ * AttestationData there (BLSGPU_ROOT_ATTESTATION_DATA, 128 B); domain_i = domains[domain_stride * i]
+ * (domain_stride 0: one domain for all). */
+#define BLSGPU_ROOT_OBJECT 0
+#define BLSGPU_ROOT_ATTESTATION_DATA 1
+int blsgpu_signing_roots(blsgpu_ctx* ctx, int kind, uint32_t n, const uint8_t* objects, uint32_t object_stride,
+                         const uint8_t* domains, uint32_t domain_stride, uint8_t* out32);
+
+/* The runtime's job sharding: part k = jobs [part_first_job[k], part_first_job[k+1]) of n_parts contiguous,
+ * cost-balanced parts (cost = sets + aggregated pubkeys / 256; set_pk_first nullable).  Pure host code. */
+int blsgpu_shard_jobs(const uint32_t* job_first_set, const uint32_t* set_pk_first, uint32_t n_jobs,
+                      uint32_t n_parts, uint32_t* part_first_job);
 
 /* "BLST_INVALID_SIZE", ... for job codes; NULL for unknown codes. */
 const char* blsgpu_code_name(int code);

@@ -2,8 +2,8 @@
 //
 // A batch group is a contiguous range of clean jobs checked with ONE final exponentiation:
 //   prod_i e(r_i pk_i, H(m_i)) * e(-g1, sum_i r_i sig_i) == 1
-// The per-set Miller loops f_i were computed by k_miller_sets; here
-//   k_group_reduce   one wave per group: S = sum r_i sig_i (G2) and F = prod f_i (Fp12), each lane a strided
+// The Miller values (per set, or per same-message unit) were computed by k_miller_acc; here
+//   k_group_reduce   one wave per group: S = sum r_i sig_i (G2) and F = prod f (Fp12), each lane a strided
 //                    partial, then a 6-level LDS tree (64 -> 1)
 //   k_group_check    one 128-lane workgroup per group: FinalExp(F * MillerLoop(-g1, S)) == 1, as
 //                    workgroup-cooperative Fp12 arithmetic (gt_wave.hpp)
@@ -27,30 +27,35 @@ __global__ __launch_bounds__(WAVE) void k_job_mask(PipelineBuffers b) {
   for (uint32_t i = a; i < e; i++) b.include[i] = err == 0 ? 1 : 0;
 }
 
-__global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const uint32_t* ranges, uint32_t ng,
-                                                       uint32_t* S_out, uint32_t* F_out) {
+__global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const uint32_t* set_ranges,
+                                                       const uint32_t* f_ranges, const uint32_t* f_src,
+                                                       bool f_per_set, uint32_t ng, uint32_t* S_out,
+                                                       uint32_t* F_out) {
   __shared__ uint32_t red[WAVE * W_FP12];
   const uint32_t g = blockIdx.x, lane = threadIdx.x;
   if (g >= ng) return;
-  const uint32_t first = ranges[2 * g], last = ranges[2 * g + 1];
-  // ---- S = sum r_i sig_i
-  g2j S = jac_infinity<fp2>();
-  for (uint32_t i = first + lane; i < last; i += WAVE)
-    if (b.include[i]) S = jac_add(S, ld_g2j(b.rsig, b.n, i));
+  // ---- S = sum r_i sig_i over the group's included sets
+  {
+    const uint32_t first = set_ranges[2 * g], last = set_ranges[2 * g + 1];
+    g2j S = jac_infinity<fp2>();
+    for (uint32_t i = first + lane; i < last; i += WAVE)
+      if (b.include[i]) S = jac_add(S, ld_g2j(b.rsig, b.n, i));
 #pragma unroll 1
-  for (int s = WAVE / 2; s >= 1; s >>= 1) {
-    if (lane >= (uint32_t)s && lane < (uint32_t)(2 * s)) st_g2j(red, WAVE, lane - s, S);
-    __syncthreads();
-    if (lane < (uint32_t)s) S = jac_add(S, ld_g2j(red, WAVE, lane));
-    __syncthreads();
+    for (int s = WAVE / 2; s >= 1; s >>= 1) {
+      if (lane >= (uint32_t)s && lane < (uint32_t)(2 * s)) st_g2j(red, WAVE, lane - s, S);
+      __syncthreads();
+      if (lane < (uint32_t)s) S = jac_add(S, ld_g2j(red, WAVE, lane));
+      __syncthreads();
+    }
+    if (lane == 0) st_g2j(S_out, ng, g, S);
   }
-  if (lane == 0) st_g2j(S_out, ng, g, S);
-  // ---- F = prod f_i
+  // ---- F = prod of the group's Miller values (per-set values: included sets only)
+  const uint32_t first = f_ranges[2 * g], last = f_ranges[2 * g + 1];
   fp12 F = fp12_one();
   bool any = false;
   for (uint32_t i = first + lane; i < last; i += WAVE)
-    if (b.include[i]) {
-      F = any ? fp12_mul(F, ld_fp12(b.f, b.n, i)) : ld_fp12(b.f, b.n, i);
+    if (!f_per_set || b.include[i]) {
+      F = any ? fp12_mul(F, ld_fp12(f_src, b.n, i)) : ld_fp12(f_src, b.n, i);
       any = true;
     }
 #pragma unroll 1
@@ -100,9 +105,11 @@ static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 void launch_job_mask(const PipelineBuffers& b, hipStream_t s) {
   if (b.n_jobs) hipLaunchKernelGGL(k_job_mask, grid_for(b.n_jobs), dim3(WAVE), 0, s, b);
 }
-void launch_group_reduce(const PipelineBuffers& b, const uint32_t* ranges, uint32_t ng, uint32_t* S, uint32_t* F,
-                         hipStream_t s) {
-  if (ng) hipLaunchKernelGGL(k_group_reduce, dim3(ng), dim3(WAVE), 0, s, b, ranges, ng, S, F);
+void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
+                         bool f_per_set, uint32_t ng, uint32_t* S, uint32_t* F, hipStream_t s) {
+  if (ng)
+    hipLaunchKernelGGL(k_group_reduce, dim3(ng), dim3(WAVE), 0, s, b, set_ranges, f_ranges,
+                       (const uint32_t*)(f_per_set ? b.f_set : b.f_unit), f_per_set, ng, S, F);
 }
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s) {
   if (ng) hipLaunchKernelGGL(k_group_check, dim3(ng), dim3(GTW_LANES), 0, s, S, F, ng, ok);

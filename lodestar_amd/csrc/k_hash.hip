@@ -1,11 +1,12 @@
-// A11 hash_to_G2 of every set's signing root, one lane per set.
+// A11 hash_to_G2, one lane per DISTINCT signing root of the call (the runtime deduplicates messages: gossip
+// attestations of one committee share AttestationData, reference chain/validation/attestation.ts:131-138).
 #include "k_common.hpp"
 
-STAGE_KERNEL void k_hash_to_g2(PipelineBuffers b, uint32_t n_sets) {
-  uint32_t i = blockIdx.x * WAVE + threadIdx.x;
-  if (i >= n_sets) return;
+STAGE_KERNEL void k_hash_to_g2(PipelineBuffers b) {
+  uint32_t u = blockIdx.x * WAVE + threadIdx.x;
+  if (u >= b.n_umsg) return;
   uint8_t msg[32];
-  const uint4* src = reinterpret_cast<const uint4*>(b.msgs + (size_t)i * 32);
+  const uint4* src = reinterpret_cast<const uint4*>(b.umsgs + (size_t)u * 32);
   uint4 m0 = src[0], m1 = src[1];
   uint32_t w[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
 #pragma unroll
@@ -17,12 +18,12 @@ STAGE_KERNEL void k_hash_to_g2(PipelineBuffers b, uint32_t n_sets) {
     a.x = fp2_zero();
     a.y = fp2_zero();
   }
-  st_g2a(b.h_aff, b.n, i, a);
-  b.flags[b.n + i] = ok ? 0 : SF_H_INF;  // hash flags: flags[n, 2n)
+  st_g2a(b.h_aff, b.nm, u, a);
+  b.mflags[u] = ok ? 0 : MF_H_INF;
 }
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
-void launch_hash_to_g2(const PipelineBuffers& b, uint32_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_hash_to_g2, grid_for(n), dim3(WAVE), 0, s, b, n);
+void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s) {
+  if (b.n_umsg) hipLaunchKernelGGL(k_hash_to_g2, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
 }

@@ -1,19 +1,68 @@
-// A4 PublicKey.aggregate over the device pubkey table, r_i * pk_i (A9), and the table upload decoder.
+// A4 PublicKey.aggregate (device pubkey table or per-key bytes), r_i * pk_i (A9), same-message unit sums,
+// aggregate serialization (PublicKey.aggregate(...).toBytes()), KeyValidate and the table upload decoder.
 #include "k_common.hpp"
 
-// One wave per set: strided partial sums of table pubkeys, then an LDS tree reduction.
+// One wave per set: strided partial sums of the set's pubkeys, then an LDS tree reduction.  Table mode reads
+// pk_table[pk_index[k]]; bytes-aggregate mode decodes pk_bytes[96 k] (trusted keys, PublicKey.fromBytes
+// without subgroup check, as the pool worker, worker.ts:110-116: an identity key adds nothing).  The first
+// malformed key (lowest k) sets the set's aggregation status; an out-of-range table index sets DEVICE_ERROR
+// (the runtime rejects such calls before launching, this is the kernel's own guard).
 __global__ __launch_bounds__(WAVE) void k_pk_aggregate(PipelineBuffers b, uint32_t n_sets) {
   __shared__ uint32_t red[WAVE * W_G1J];
+  __shared__ uint32_t err_k[WAVE];
+  __shared__ int32_t err_c[WAVE];
   uint32_t set = blockIdx.x;
   uint32_t lane = threadIdx.x;
   if (set >= n_sets) return;
-  uint32_t first = b.set_pk_first[set], last = b.set_pk_first[set + 1];
+  int8_t* agg_status = b.status + 2 * b.n;
+  const uint32_t first = b.set_pk_first[set], last = b.set_pk_first[set + 1];
   g1j acc = jac_infinity<fp>();
+  uint32_t my_err_k = 0xffffffffu;
+  int my_err = 0;
   for (uint32_t k = first + lane; k < last; k += WAVE) {
-    uint32_t idx = b.pk_index[k];
-    if (idx < b.pk_table_n) acc = jac_add_aff(acc, ld_pktab(b.pk_table, idx));
+    g1a q;
+    if (b.pk_bytes) {
+      uint8_t raw[96];
+      const uint8_t* src = b.pk_bytes + (size_t)k * 96;
+#pragma unroll
+      for (int t = 0; t < 96; t++) raw[t] = src[t];
+      bool inf = false;
+      const int st = pk_decode96(raw, q, inf);
+      if (st != BLS_OK) {
+        if (my_err == 0) {
+          my_err = st;
+          my_err_k = k;
+        }
+        continue;
+      }
+      if (inf) continue;
+    } else {
+      const uint32_t idx = b.pk_index[k];
+      if (idx >= b.pk_table_n) {
+        if (my_err == 0) {
+          my_err = BLS_DEVICE_ERROR;
+          my_err_k = k;
+        }
+        continue;
+      }
+      q = ld_pktab(b.pk_table, idx);
+    }
+    acc = jac_add_aff(acc, q);
   }
-  uint32_t cnt = last - first;
+  err_k[lane] = my_err_k;
+  err_c[lane] = my_err;
+  __syncthreads();
+  if (lane == 0) {
+    uint32_t bk = 0xffffffffu;
+    int bc = 0;
+    for (int l = 0; l < WAVE; l++)
+      if (err_k[l] < bk) {
+        bk = err_k[l];
+        bc = err_c[l];
+      }
+    agg_status[set] = (int8_t)bc;
+  }
+  const uint32_t cnt = last - first;
   if (cnt <= 1) {  // nothing to reduce
     if (lane == 0) st_g1j(b.pk_jac, b.n, set, acc);
     return;
@@ -44,15 +93,9 @@ __global__ __launch_bounds__(WAVE) void k_pk_aggregate(PipelineBuffers b, uint32
   if (lane == 0) st_g1j(b.pk_jac, b.n, set, acc);
 }
 
-// r_i * pk_i -> affine.  Bytes mode decodes the 96-byte pubkey; table mode reads k_pk_aggregate's sum.
-// pk statuses go to their own array (status[n, 2n)); the host gives them precedence over signature
-// statuses because the reference deserializes pubkeys first (worker.ts:39).
-STAGE_KERNEL void k_pk_finish(PipelineBuffers b, uint32_t n_sets, int8_t* pk_status) {
-  uint32_t i = blockIdx.x * WAVE + threadIdx.x;
-  if (i >= n_sets) return;
-  int st = BLS_OK;
-  g1j P;
-  if (b.pk_bytes) {
+// The set's (aggregated) public key as a Jacobian point + status.  Single-key bytes mode decodes pk_bytes.
+__device__ __forceinline__ int set_pubkey(const PipelineBuffers& b, uint32_t i, g1j& P) {
+  if (b.pk_bytes && !b.set_pk_first) {
     uint8_t raw[96];
     const uint4* src = reinterpret_cast<const uint4*>(b.pk_bytes + (size_t)i * 96);
 #pragma unroll
@@ -64,18 +107,25 @@ STAGE_KERNEL void k_pk_finish(PipelineBuffers b, uint32_t n_sets, int8_t* pk_sta
     }
     g1a a;
     bool inf = false;
-    st = pk_decode96(raw, a, inf);
+    int st = pk_decode96(raw, a, inf);
     if (st == BLS_OK && inf) st = BLS_PK_IS_INFINITY;
     if (st == BLS_OK) P = jac_from_aff(a);
-  } else {
-    uint32_t cnt = b.set_pk_first[i + 1] - b.set_pk_first[i];
-    if (cnt == 0) {
-      st = BLS_EMPTY_AGGREGATE;
-    } else {
-      P = ld_g1j(b.pk_jac, b.n, i);
-      if (jac_is_inf(P)) st = BLS_PK_IS_INFINITY;
-    }
+    return st;
   }
+  if (b.set_pk_first[i + 1] == b.set_pk_first[i]) return BLS_EMPTY_AGGREGATE;
+  const int st = b.status[2 * b.n + i];
+  if (st) return st;
+  P = ld_g1j(b.pk_jac, b.n, i);
+  return jac_is_inf(P) ? BLS_PK_IS_INFINITY : BLS_OK;
+}
+
+// r_i * pk_i -> affine.  pk statuses go to their own array (status[n, 2n)); the job mask gives them
+// precedence over signature statuses because the reference deserializes pubkeys first (worker.ts:39).
+STAGE_KERNEL void k_pk_finish(PipelineBuffers b, uint32_t n_sets, int8_t* pk_status) {
+  uint32_t i = blockIdx.x * WAVE + threadIdx.x;
+  if (i >= n_sets) return;
+  g1j P;
+  int st = set_pubkey(b, i, P);
   g1a out;
   out.x = fp_zero();
   out.y = fp_zero();
@@ -86,6 +136,75 @@ STAGE_KERNEL void k_pk_finish(PipelineBuffers b, uint32_t n_sets, int8_t* pk_sta
   }
   st_g1a(b.pk_aff, b.n, i, out);
   pk_status[i] = (int8_t)st;
+}
+
+// Same-message merging: P_u = sum of r_i pk_i over the unit's included sets (lane per unit).
+STAGE_KERNEL void k_unit_aggregate(PipelineBuffers b) {
+  uint32_t u = blockIdx.x * WAVE + threadIdx.x;
+  if (u >= b.n_units) return;
+  const uint32_t a = b.unit_set_first[u], e = b.unit_set_first[u + 1];
+  g1a out;
+  out.x = fp_zero();
+  out.y = fp_zero();
+  bool ok = false;
+  if (e - a == 1) {
+    const uint32_t i = b.unit_sets[a];
+    if (b.include[i]) {
+      out = ld_g1a(b.pk_aff, b.n, i);
+      ok = true;
+    }
+  } else {
+    g1j acc = jac_infinity<fp>();
+    for (uint32_t k = a; k < e; k++) {
+      const uint32_t i = b.unit_sets[k];
+      if (b.include[i]) acc = jac_add_aff(acc, ld_g1a(b.pk_aff, b.n, i));
+    }
+    ok = jac_to_aff(acc, out);  // the identity (all excluded) pairs to 1
+  }
+  st_g1a(b.unit_p, b.n, u, out);
+  b.unit_ok[u] = ok ? 1 : 0;
+}
+
+// PublicKey.aggregate(pks).toBytes(): 96-byte uncompressed or 48-byte compressed, per set.  status[3n...]
+// receives 0 / EMPTY_AGGREGATE / a key error; an aggregate equal to the identity encodes the identity.
+__global__ __launch_bounds__(WAVE) void k_pk_serialize(PipelineBuffers b, uint32_t n_sets, uint8_t* out,
+                                                       uint32_t out_len) {
+  uint32_t i = blockIdx.x * WAVE + threadIdx.x;
+  if (i >= n_sets) return;
+  int st = b.set_pk_first[i + 1] == b.set_pk_first[i] ? BLS_EMPTY_AGGREGATE : b.status[2 * b.n + i];
+  uint8_t buf[96];
+  for (int k = 0; k < 96; k++) buf[k] = 0;
+  if (st == BLS_OK) {
+    g1a a;
+    if (!jac_to_aff(ld_g1j(b.pk_jac, b.n, i), a)) {
+      buf[0] = out_len == 48 ? 0xc0 : 0x40;
+    } else if (out_len == 48) {
+      g1a_compress(a, buf);
+    } else {
+      g1a_to_be96(a, buf);
+    }
+  }
+  uint8_t* o = out + (size_t)i * out_len;
+  for (uint32_t k = 0; k < out_len; k++) o[k] = buf[k];
+  b.status[i] = (int8_t)st;
+}
+
+// KeyValidate of untrusted pubkeys, one lane per key -> 96-byte uncompressed + status.
+__global__ __launch_bounds__(WAVE) void k_key_validate(const uint8_t* pks, uint32_t n, uint32_t pk_len, uint32_t stride,
+                                                       uint8_t* out96, int8_t* status) {
+  uint32_t i = blockIdx.x * WAVE + threadIdx.x;
+  if (i >= n) return;
+  uint8_t raw[96];
+  const uint8_t* src = pks + (size_t)i * stride;
+  for (uint32_t k = 0; k < 96; k++) raw[k] = k < pk_len ? src[k] : 0;
+  g1a a;
+  const int st = pk_key_validate(raw, pk_len, a);
+  uint8_t buf[96];
+  for (int k = 0; k < 96; k++) buf[k] = 0;
+  if (st == BLS_OK) g1a_to_be96(a, buf);
+  if (out96)
+    for (int k = 0; k < 96; k++) out96[(size_t)i * 96 + k] = buf[k];
+  status[i] = (int8_t)st;
 }
 
 __global__ __launch_bounds__(WAVE) void k_pk_table_fill(const uint8_t* pk96, uint32_t n, uint32_t* table_dst,
@@ -116,8 +235,18 @@ void launch_pk_aggregate(const PipelineBuffers& b, uint32_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_pk_aggregate, dim3(n), dim3(WAVE), 0, s, b, n);
 }
 void launch_pk_finish(const PipelineBuffers& b, uint32_t n, hipStream_t s) {
-  // pk status lives right after the set status array (runtime allocates 2 * stride bytes)
+  // pk status lives right after the set status array (runtime allocates 3 * stride bytes)
   if (n) hipLaunchKernelGGL(k_pk_finish, grid_for(n), dim3(WAVE), 0, s, b, n, b.status + b.n);
+}
+void launch_unit_aggregate(const PipelineBuffers& b, hipStream_t s) {
+  if (b.n_units) hipLaunchKernelGGL(k_unit_aggregate, grid_for(b.n_units), dim3(WAVE), 0, s, b);
+}
+void launch_pk_serialize(const PipelineBuffers& b, uint32_t n, uint8_t* out, uint32_t out_len, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_pk_serialize, grid_for(n), dim3(WAVE), 0, s, b, n, out, out_len);
+}
+void launch_key_validate(const uint8_t* pks, uint32_t n, uint32_t pk_len, uint32_t stride, uint8_t* out96,
+                         int8_t* status, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_key_validate, grid_for(n), dim3(WAVE), 0, s, pks, n, pk_len, stride, out96, status);
 }
 void launch_pk_table_fill(const uint8_t* pk96, uint32_t n, uint32_t* table_dst, int8_t* status, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_pk_table_fill, grid_for(n), dim3(WAVE), 0, s, pk96, n, table_dst, status);

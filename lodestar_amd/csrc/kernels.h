@@ -12,57 +12,91 @@
 #define W_FP12 (12 * W_FP)
 // Pubkey table entries: AoS, 32 words (x limbs, y limbs, pad) = one 128-byte line per key
 #define W_PKTAB 32
+// Miller-loop line coefficients per message: 68 steps x (l0, c1, c4)
+#define MILLER_STEPS 68
+#define W_LINE (3 * 2 * W_FP)
 
 // set flags (uint8 per set)
 #define SF_SIG_INF 1u
-#define SF_H_INF 2u
-#define SF_PK_INF 4u
+// per-message flags
+#define MF_H_INF 1u
 
 struct PipelineBuffers {
-  uint32_t n;  // SoA stride (>= n_sets)
-  // inputs
+  uint32_t n;  // SoA stride of per-set arrays (>= n_sets)
+  // ---- inputs
   const uint8_t* sigs;
   const uint32_t* sig_len;
   uint32_t sig_stride;
-  const uint8_t* msgs;
-  const uint8_t* pk_bytes;       // bytes mode or nullptr
-  const uint32_t* set_pk_first;  // table mode
+  // public keys: pk_bytes && !set_pk_first: one 96-B key per set; pk_bytes && set_pk_first: set i aggregates
+  // keys [set_pk_first[i], set_pk_first[i+1]) of pk_bytes; !pk_bytes: table entries pk_index[...]
+  const uint8_t* pk_bytes;
+  const uint32_t* set_pk_first;
   const uint32_t* pk_index;
   const uint32_t* pk_table;  // AoS W_PKTAB words per key
   uint32_t pk_table_n;
   const uint64_t* scalars;
   const uint32_t* job_first_set;  // [n_jobs + 1], shard-relative
   uint32_t n_jobs;
-  // intermediates
-  uint32_t* sig_aff;  // W_G2A
-  uint32_t* h_aff;    // W_G2A
-  uint32_t* pk_jac;   // W_G1J (table mode aggregate)
-  uint32_t* pk_aff;   // W_G1A (r * pk)
-  uint32_t* rsig;     // W_G2J
-  uint32_t* f;        // W_FP12
-  uint32_t* lines;    // Miller lines: MILLER_STEPS x 3 Fp2 (6 * W_FP words) per set, step-major SoA
-  uint8_t* flags;     // [2n]: sig flags, hash flags
-  int8_t* status;     // [2n]: signature status, pubkey status
+  // messages, deduplicated per call: set i signs umsgs[msg_idx[i]]
+  const uint8_t* umsgs;
+  const uint32_t* msg_idx;
+  uint32_t n_umsg;
+  uint32_t nm;  // SoA stride of per-message arrays (>= n_umsg)
+  // pairing units (same-message merging): unit u = the included sets unit_sets[unit_set_first[u] ..
+  // unit_set_first[u+1]) of one batch group, all signing umsgs[unit_msg[u]]; P_u = sum r_i pk_i
+  uint32_t n_units;
+  const uint32_t* unit_set_first;
+  const uint32_t* unit_sets;
+  const uint32_t* unit_msg;
+  // ---- intermediates
+  uint32_t* sig_aff;  // W_G2A, per set
+  uint32_t* h_aff;    // W_G2A, per message
+  uint32_t* pk_jac;   // W_G1J, per set (aggregate)
+  uint32_t* pk_aff;   // W_G1A, per set (r * pk, affine)
+  uint32_t* rsig;     // W_G2J, per set
+  uint32_t* unit_p;   // W_G1A, per unit (stride n)
+  uint32_t* f_set;    // W_FP12, per set: Miller values (per-set mode and the fallback)
+  uint32_t* f_unit;   // W_FP12, per unit (stride n)
+  uint32_t* lines;    // Miller lines, per message: MILLER_STEPS x W_LINE words, step-major SoA (stride nm)
+  uint8_t* flags;     // [n]: sig flags
+  uint8_t* mflags;    // [nm]: message flags
+  uint8_t* unit_ok;   // [n]: unit has a finite P_u
+  int8_t* status;     // [3n]: signature status, pubkey status, aggregation status
   int8_t* job_err;    // [n_jobs]: first pubkey/signature error of the job (0 = clean)
   uint8_t* include;   // [n]: set belongs to a clean job (enters the batch equation)
 };
 
 void launch_sig_decode(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
-void launch_hash_to_g2(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
+void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s);  // over the unique messages
 void launch_pk_aggregate(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 void launch_pk_finish(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 void launch_sig_scale(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
-void launch_miller_sets(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 // per-job error status and the per-set include mask of the batch equation
 void launch_job_mask(const PipelineBuffers& b, hipStream_t s);
-// Batch groups: group g covers sets [ranges[2g], ranges[2g+1]) (only included sets count).
-// reduce: S_g = sum r_i sig_i (W_G2J SoA, stride n_groups), F_g = prod f_i (W_FP12 SoA, stride n_groups)
-void launch_group_reduce(const PipelineBuffers& b, const uint32_t* ranges, uint32_t n_groups, uint32_t* S,
-                         uint32_t* F, hipStream_t s);
+// P_u = sum over the unit's included sets of r_i pk_i (affine)
+void launch_unit_aggregate(const PipelineBuffers& b, hipStream_t s);
+// Miller lines of every unique message
+void launch_miller_lines(const PipelineBuffers& b, hipStream_t s);
+// Miller values: units (f_unit) when `units`, else per set (f_set) for n sets -- all sets when set_list is
+// null, else the listed ones
+void launch_miller_acc(const PipelineBuffers& b, bool units, uint32_t n, const uint32_t* set_list, hipStream_t s);
+// Batch groups: group g covers sets [set_ranges[2g], set_ranges[2g+1]) (S over included sets) and Miller
+// values [f_ranges[2g], f_ranges[2g+1]) of f (per-set values count only for included sets when f_per_set).
+// reduce: S_g = sum r_i sig_i (W_G2J SoA, stride n_groups), F_g = prod f (W_FP12 SoA, stride n_groups)
+void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
+                         bool f_per_set, uint32_t n_groups, uint32_t* S, uint32_t* F, hipStream_t s);
 // check: ok_g = FinalExp(F_g * MillerLoop(-g1, S_g)) == 1
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t n_groups, uint8_t* ok, hipStream_t s);
 // pubkey table upload: decode 96-byte affine encodings into table entries, per-entry status
 void launch_pk_table_fill(const uint8_t* pk96, uint32_t n, uint32_t* table_dst, int8_t* status, hipStream_t s);
+// serialize the per-set aggregate (pk_jac) to 96-byte uncompressed or 48-byte compressed encodings
+void launch_pk_serialize(const PipelineBuffers& b, uint32_t n_sets, uint8_t* out, uint32_t out_len, hipStream_t s);
+// KeyValidate of untrusted 48/96-byte pubkeys (decode + G1 subgroup check) -> 96-byte uncompressed
+void launch_key_validate(const uint8_t* pks, uint32_t n, uint32_t pk_len, uint32_t stride, uint8_t* out96,
+                         int8_t* status, hipStream_t s);
+// SSZ signing roots (SigningData / AttestationData hash_tree_root)
+void launch_signing_roots(int kind, const uint8_t* in, uint32_t n, uint32_t in_stride, const uint8_t* domain,
+                          uint32_t domain_stride, uint8_t* out, hipStream_t s);
 // debug ops (blsgpu_debug_op)
 void launch_debug_op(int op, uint32_t n, const uint8_t* in, uint32_t in_stride, uint8_t* out, uint32_t out_stride,
                      int32_t* status, hipStream_t s);

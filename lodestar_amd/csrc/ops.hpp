@@ -99,6 +99,56 @@ BLS_HDNI int pk_decode96(const uint8_t* b, g1a& out, bool& inf) {
   return BLS_OK;
 }
 
+// G1 subgroup check for KeyValidate: phi(P) == -[z^2]P with phi(x, y) = (beta x, y) (Scott, eprint
+// 2021/1130; the definitional [r]P == O is the oracle's, tests/test_emu_logic.py compares the two).
+BLS_HDNI bool g1_in_subgroup(const g1a& p) {
+  g1j P = jac_from_aff(p);
+  g1j z2P = jac_mul_zabs(jac_mul_zabs(P));  // [z^2]P (z^2 > 0)
+  g1j phi = P;
+  phi.x = fp_mul(p.x, G1_BETA);
+  return jac_eq(phi, jac_neg(z2P));
+}
+
+// Decompress a 48-byte G1 encoding (blst POINTonE1_Uncompress semantics); no subgroup check.
+BLS_HDNI int pk_decode48(const uint8_t* b, g1a& out, bool& inf) {
+  inf = false;
+  const uint8_t b0 = b[0];
+  if (!(b0 & 0x80)) return BLS_BAD_ENCODING;
+  if (b0 & 0x40) {
+    if ((b0 & 0x3f) == 0 && bytes_all_zero(b + 1, 47)) {
+      inf = true;
+      return BLS_OK;
+    }
+    return BLS_BAD_ENCODING;
+  }
+  fp x;
+  if (!fp_from_be48_plain(b, x, 0x1f)) return BLS_BAD_ENCODING;
+  out.x = fp_to_mont(x);
+  const fp rhs = fp_add(fp_mul(fp_sqr(out.x), out.x), FP_B1);
+  fp y = fp_mul(rhs, fp_pow_p34(rhs));  // rhs^((p+1)/4)
+  if (!fp_eq(fp_sqr(y), rhs)) return BLS_POINT_NOT_ON_CURVE;
+  const bool largest = fp_plain_gt_half(fp_from_mont(y));
+  if (largest != ((b0 & 0x20) != 0)) y = fp_neg(y);
+  out.y = y;
+  return BLS_OK;
+}
+
+// KeyValidate (PublicKey.fromBytes(pk, validate = true): processDeposit.ts:56-64, spec bls.ts:33-42):
+// 48- or 96-byte encoding, not the identity, in G1.
+BLS_HDNI int pk_key_validate(const uint8_t* b, uint32_t len, g1a& out) {
+  bool inf = false;
+  int st;
+  if (len == 48)
+    st = pk_decode48(b, out, inf);
+  else if (len == 96)
+    st = pk_decode96(b, out, inf);
+  else
+    return BLS_INVALID_SIZE;
+  if (st != BLS_OK) return st;
+  if (inf) return BLS_PK_IS_INFINITY;
+  return g1_in_subgroup(out) ? BLS_OK : BLS_POINT_NOT_IN_GROUP;
+}
+
 BLS_HD void fp_to_be48(const fp& mont, uint8_t* b) { fp_to_be48_plain(fp_from_mont(mont), b); }
 
 BLS_HD void g2a_to_be192(const g2a& p, uint8_t* b) {
@@ -110,6 +160,13 @@ BLS_HD void g2a_to_be192(const g2a& p, uint8_t* b) {
 BLS_HD void g1a_to_be96(const g1a& p, uint8_t* b) {
   fp_to_be48(p.x, b);
   fp_to_be48(p.y, b + 48);
+}
+
+// ZCash compressed encoding of an affine G1 point (not infinity)
+BLS_HD void g1a_compress(const g1a& p, uint8_t* b) {
+  fp_to_be48(p.x, b);
+  const bool largest = fp_plain_gt_half(fp_from_mont(p.y));
+  b[0] |= 0x80 | (largest ? 0x20 : 0);
 }
 
 // ZCash compressed encoding of an affine G2 point (not infinity)

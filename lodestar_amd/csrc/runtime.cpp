@@ -2,32 +2,33 @@
 //
 // Replaces BlsMultiThreadWorkerPool's job plumbing (reference packages/beacon-node/src/chain/bls/
 // multithread/index.ts:134-412) and the worker's batch/fallback policy (multithread/worker.ts:32-108)
-// with HIP streams on MI355X and no worker threads doing arithmetic:
-//   * jobs are sharded across devices in contiguous, cost-balanced ranges (never splitting a job);
-//   * each device owns several "slots" (a HIP stream + its staging and work buffers).  A call takes one
-//     free slot per device it uses, so independent verifySignatureSets calls run concurrently on the
-//     GPU -- the way the reference keeps all its workers busy -- and the device is filled by several
-//     batches' lane-per-set kernels at once;
-//   * each shard runs the stage kernels (k_*.hip): signature decode + subgroup check, hash_to_G2,
-//     pubkey aggregation, r_i scaling, per-set Miller loops, then the batch-group tail;
+// with HIP streams on MI355X and no host threads doing arithmetic:
+//   * a call (one verifySignatureSets submission) is split into contiguous, cost-balanced shards of jobs,
+//     one per device it uses (never splitting a job); shards go to their device's task queue;
+//   * each device owns several slots (a HIP stream + its staging and work buffers) and ONE long-lived
+//     dispatcher thread per slot that takes shards from the device queue, so concurrent calls overlap on
+//     the GPU -- the way the reference keeps all its workers busy -- with no thread created per call;
+//   * each shard runs the stage kernels (k_*.hip): signature decode + subgroup check, hash_to_G2 of every
+//     DISTINCT signing root, pubkey aggregation, r_i scaling, the job mask, same-message unit sums, Miller
+//     loops (per set, or per (group, message) unit), then the batch-group tail;
 //   * batchable jobs are packed into groups of >= group_sets sets (random linear combination, one final
-//     exponentiation per group); non-batchable jobs are their own group; a single-set non-batchable
-//     job uses r = 1 (= CoreVerify, maybeBatch.ts:34-38);
-//   * a failed group with several clean jobs is split into <= 8 contiguous sub-ranges that are re-checked
-//     with the same group kernels (k-ary bisection) until every job is resolved on its own.  The per-set
-//     Miller loops stay on the device, so a re-check costs one Miller loop + final exponentiation.
-//     Per job the answer is the reference's: valid iff every set of the job verifies (worker.ts:76-98).
+//     exponentiation per group); non-batchable jobs are their own group; a single-set non-batchable job
+//     uses r = 1 (= CoreVerify, maybe_batch.ts:34-38);
+//   * a failed group is resolved by ONE parallel launch that re-checks every clean job of every failed
+//     group on its own (the reference re-verifies each job of a failed chunk, worker.ts:76-98): per job the
+//     answer is the reference's, valid iff every set of the job verifies.
 // There is no CPU verification path: without a usable GPU blsgpu_init fails.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <string.h>
 #include <stdlib.h>
+#include <string.h>
 #include <sys/random.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
@@ -87,78 +88,50 @@ struct HostBuf {  // pinned staging
 };
 
 constexpr int kStages = 8;
-constexpr size_t kMillerLineWords = 68 * 6 * W_FP;  // MILLER_STEPS x (l0, c1, c4) per set (k_miller.hip)
+constexpr size_t kMillerLineWords = (size_t)MILLER_STEPS * W_LINE;
 
-// One in-flight batch on one device: a stream and every per-call buffer.
+inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// One in-flight shard on one device: a stream and every per-call buffer.
 struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev[kStages + 1] = {};
   // d_in / h_in: every per-call input packed into one arena (one H2D transfer); d_res / h_res: job errors +
-  // group verdicts (one D2H transfer).  Each transfer is a blit kernel that must find a free SIMD among
-  // the full-register-file verification waves, so a batch pays for each one in queueing delay.
-  DevBuf<uint8_t> d_in, d_res, d_flags, d_ok, d_include;
-  DevBuf<int8_t> d_status;
-  DevBuf<uint32_t> d_ranges, d_work, d_S, d_F, d_lines;
+  // group verdicts (one D2H transfer).
+  DevBuf<uint8_t> d_in, d_res, d_bytes, d_ok;
+  DevBuf<uint32_t> d_work, d_lines, d_S, d_F, d_list;
   HostBuf<uint8_t> h_in, h_res, h_ok;
-  HostBuf<uint32_t> h_ranges;
+  HostBuf<uint32_t> h_list;
 
   void release_all() {
-    d_in.release(); d_res.release(); d_flags.release(); d_ok.release(); d_include.release(); d_status.release();
-    d_ranges.release(); d_work.release(); d_S.release(); d_F.release(); d_lines.release();
-    h_in.release(); h_res.release(); h_ok.release(); h_ranges.release();
+    d_in.release(); d_res.release(); d_bytes.release(); d_ok.release();
+    d_work.release(); d_lines.release(); d_S.release(); d_F.release(); d_list.release();
+    h_in.release(); h_res.release(); h_ok.release(); h_list.release();
   }
+};
+
+struct Call;
+struct Task {
+  Call* call;
+  uint32_t shard;
 };
 
 struct Device {
   int id = 0;
-  hipStream_t table_stream = nullptr;
+  hipStream_t table_stream = nullptr;  // uploads and the synchronous helpers (debug, aggregate, ...)
+  std::mutex helper_mu;
+  Slot helper;  // buffers of the synchronous helpers (on table_stream)
   // pubkey table (AoS, W_PKTAB words per key): verification holds it shared, uploads exclusive
   std::shared_mutex table_mu;
   DevBuf<uint32_t> table;
   uint32_t table_n = 0;
-  // slots
-  std::mutex slot_mu;
-  std::condition_variable slot_cv;
+  // slots, each served by one dispatcher thread taking tasks from this device's queue
+  std::mutex q_mu;
+  std::condition_variable q_cv;
+  std::deque<Task> queue;
+  bool stop = false;
   std::vector<Slot*> slots;
-  std::vector<Slot*> free_slots;
-
-  void add_slot() {
-    Slot* s = new Slot();
-    HIPCHK(hipSetDevice(id));
-    HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
-    slots.push_back(s);
-    free_slots.push_back(s);
-  }
-  Slot* acquire() {
-    std::unique_lock<std::mutex> lk(slot_mu);
-    slot_cv.wait(lk, [&] { return !free_slots.empty(); });
-    Slot* s = free_slots.back();
-    free_slots.pop_back();
-    return s;
-  }
-  void release(Slot* s) {
-    {
-      std::lock_guard<std::mutex> lk(slot_mu);
-      free_slots.push_back(s);
-    }
-    slot_cv.notify_one();
-  }
-  void destroy_all() {
-    (void)hipSetDevice(id);
-    for (Slot* s : slots) {
-      if (s->stream) (void)hipStreamSynchronize(s->stream);
-      s->release_all();
-      for (auto& e : s->ev)
-        if (e) (void)hipEventDestroy(e);
-      if (s->stream) (void)hipStreamDestroy(s->stream);
-      delete s;
-    }
-    slots.clear();
-    free_slots.clear();
-    table.release();
-    if (table_stream) (void)hipStreamDestroy(table_stream);
-  }
+  std::vector<std::thread> workers;
 };
 
 inline uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
@@ -170,60 +143,144 @@ inline uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
   return z ? z : 1;
 }
 
-}  // namespace
-
-struct blsgpu_ctx {
-  std::vector<Device*> devs;
-  std::atomic<bool> closed{false};
-  std::atomic<int> inflight{0};
-  std::mutex async_mu;
-  std::condition_variable async_cv;
-  std::mutex table_mu;
-  std::mutex opt_mu;
+struct Options {  // snapshot taken at the start of each call
   int64_t group_sets = 256;
   int64_t max_devices = 64;
-  int64_t split_ways = 8;
   bool profile = false;
+  bool dedupe = true;
 };
-
-namespace {
 
 struct Shard {
   uint32_t job_begin, job_end;  // job range
   uint32_t set_begin, set_end;  // set range
 };
 
+// Inputs owned by an asynchronous call (the caller may reuse its buffers once blsgpu_submit returns)
+struct Owned {
+  std::vector<uint32_t> jfs, siglen, pkfirst, pkidx;
+  std::vector<uint8_t> jflags, pkb, msgs, sigs;
+};
+
+struct Call {
+  blsgpu_ctx* ctx = nullptr;
+  blsgpu_batch b{};
+  Owned* owned = nullptr;
+  int8_t* job_result = nullptr;
+  blsgpu_stats* stats = nullptr;
+  uint64_t seed = 0;
+  uint32_t max_index = 0;  // largest pubkey-table index of the call (table mode)
+  Options opt;
+  std::vector<Shard> shards;
+  std::vector<blsgpu_stats> sst;
+  std::vector<int> rc;
+  std::atomic<uint32_t> remaining{0};
+  std::chrono::steady_clock::time_point t0;
+  // completion: async callback, or a waiting synchronous caller
+  blsgpu_done_cb done = nullptr;
+  void* user = nullptr;
+  bool sync = false;
+  std::mutex m;
+  std::condition_variable cv;
+  bool finished = false;
+  int status = BLSGPU_OK;
+};
+
+}  // namespace
+
+struct blsgpu_ctx {
+  std::vector<Device*> devs;
+  std::atomic<bool> closed{false};
+  std::mutex active_mu;  // calls in progress (sync and async): destroy waits for zero
+  std::condition_variable active_cv;
+  int active = 0;
+  std::mutex table_mu;  // serializes uploads
+  std::mutex opt_mu;
+  Options opt;
+  int64_t slots_per_device = 4;
+};
+
+namespace {
+
+// ---- contiguous cost-balanced sharding (the rule lodestar_amd/shard.py restates) ------------------------
+// cost of a job = its sets + 1/256 per aggregated pubkey; part k ends at the largest job boundary whose
+// prefix cost is <= total (k+1)/n_parts; the last part takes the rest.
+void shard_rule(const uint32_t* jfs, const uint32_t* spf, uint32_t n_jobs, uint32_t n_parts, uint32_t* out) {
+  const uint32_t n_sets = n_jobs ? jfs[n_jobs] : 0;
+  std::vector<double> set_prefix(n_sets + 1, 0.0);
+  for (uint32_t i = 0; i < n_sets; i++)
+    set_prefix[i + 1] = set_prefix[i] + 1.0 + (spf ? (double)(spf[i + 1] - spf[i]) / 256.0 : 0.0);
+  std::vector<double> cost(n_jobs + 1);
+  for (uint32_t j = 0; j <= n_jobs; j++) cost[j] = set_prefix[n_jobs ? jfs[j] : 0];
+  uint32_t j0 = 0;
+  out[0] = 0;
+  for (uint32_t k = 0; k < n_parts; k++) {
+    uint32_t j1;
+    if (k + 1 == n_parts) {
+      j1 = n_jobs;
+    } else {
+      const double target = cost[n_jobs] * (k + 1) / n_parts;
+      // largest j1 >= j0 with cost[j1] <= target
+      j1 = (uint32_t)(std::upper_bound(cost.begin(), cost.end(), target) - cost.begin());
+      j1 = j1 ? j1 - 1 : 0;
+      j1 = std::max(j0, j1);
+    }
+    out[k + 1] = j1;
+    j0 = j1;
+  }
+}
+
+// ---- message deduplication: open addressing on the 32-byte signing roots ----------------------------------
+struct MsgIndex {
+  std::vector<uint32_t> slot;  // 1 + unique index, 0 = empty
+  uint64_t key;
+  explicit MsgIndex(uint32_t n, uint64_t k) : key(k) {
+    size_t cap = 16;
+    while (cap < (size_t)n * 2) cap <<= 1;
+    slot.assign(cap, 0);
+  }
+  static uint64_t mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  // returns the unique index of msg; appends to `uniq` (set indices of first occurrences) when new
+  uint32_t find_or_add(const uint8_t* msgs, uint32_t i, std::vector<uint32_t>& uniq) {
+    uint64_t w[4];
+    memcpy(w, msgs + (size_t)i * 32, 32);
+    const size_t mask = slot.size() - 1;
+    size_t h = (size_t)(mix(w[0] ^ key) ^ mix(w[1] + key) ^ w[2] ^ (w[3] << 1)) & mask;
+    for (;;) {
+      const uint32_t s = slot[h];
+      if (!s) {
+        uniq.push_back(i);
+        slot[h] = (uint32_t)uniq.size();
+        return (uint32_t)uniq.size() - 1;
+      }
+      if (memcmp(msgs + (size_t)uniq[s - 1] * 32, msgs + (size_t)i * 32, 32) == 0) return s - 1;
+      h = (h + 1) & mask;
+    }
+  }
+};
+
 // Runs one device's shard on one slot.  Writes job_result[job_begin..job_end).
-int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_t* job_result,
-              uint64_t seed, blsgpu_stats& st) {
+int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_t* job_result, uint64_t seed,
+              const Options& opt, uint32_t max_index, blsgpu_stats& st) {
   const uint32_t n = sh.set_end - sh.set_begin;
   const uint32_t nj = sh.job_end - sh.job_begin;
   if (nj == 0) return BLSGPU_OK;
   HIPCHK(hipSetDevice(d.id));
   const uint32_t s0 = sh.set_begin;
   const uint32_t stride = std::max<uint32_t>(n, 1);
-  const uint32_t split_ways = (uint32_t)std::max<int64_t>(2, ctx->split_ways);
-
-  // ---- host-side job structure: groups (contiguous job ranges), scalars ------------------------
-  // Non-batchable jobs are groups of their own; consecutive batchable jobs are packed until a group
-  // holds >= group_sets sets.  Empty jobs get no group (rejected with EMPTY_SET).
-  // Input arena layout (256-B aligned sections; groups <= jobs bounds the ranges section):
-  //   scalars n*8 | job_first_set (nj+1)*4 | sigs n*192 | sig_len n*4 | msgs n*32 | ranges nj*8 |
-  //   table mode: set_pk_first (n+1)*4, pk_index npk*4;  bytes mode: pk_bytes n*96
   const bool table_mode = b.pk_bytes == nullptr;
-  const uint32_t npk = table_mode ? b.set_pk_first[sh.set_end] - b.set_pk_first[s0] : 0;
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t o_scal = 0, o_jobs = al(o_scal + (size_t)n * 8), o_sigs = al(o_jobs + (size_t)(nj + 1) * 4),
-               o_siglen = al(o_sigs + (size_t)n * 192), o_msgs = al(o_siglen + (size_t)n * 4),
-               o_ranges = al(o_msgs + (size_t)n * 32), o_pk = al(o_ranges + (size_t)nj * 8),
-               o_pkidx = al(o_pk + (size_t)(n + 1) * 4),
-               in_bytes = table_mode ? o_pkidx + (size_t)npk * 4 : o_pk + (size_t)n * 96;
-  sl.h_in.ensure(in_bytes);
-  sl.d_in.ensure(in_bytes);
-  uint8_t* const hin = sl.h_in.p;
-  uint64_t* scal = reinterpret_cast<uint64_t*>(hin + o_scal);
-  uint32_t* hjobs = reinterpret_cast<uint32_t*>(hin + o_jobs);
-  std::vector<uint32_t> job_group(nj, UINT32_MAX);
+  const bool bytes_agg = b.pk_bytes && b.set_pk_first;
+  const uint32_t pk_base = b.set_pk_first ? b.set_pk_first[s0] : 0;
+  const uint32_t npk = b.set_pk_first ? b.set_pk_first[sh.set_end] - pk_base : 0;
+  // the device's table must hold every index of the call (checked per device, under its table lock: a
+  // call may race an upload that has reached some devices only)
+  if (table_mode && npk && max_index >= d.table_n) return BLSGPU_ERR_ARGS;
+
+  // ---- host-side job structure: groups (contiguous job ranges), scalars ------------------------------------
+  std::vector<uint64_t> scal(n);
   std::vector<std::pair<uint32_t, uint32_t>> group_jobs;  // [first job, end job) (shard-relative)
   {
     uint32_t cur_sets = 0;
@@ -231,14 +288,12 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
     for (uint32_t j = 0; j < nj; j++) {
       const uint32_t gj = sh.job_begin + j;
       const uint32_t a = b.job_first_set[gj] - s0, e = b.job_first_set[gj + 1] - s0;
-      hjobs[j] = a;
       const bool batchable = b.job_flags && (b.job_flags[gj] & 1u);
       if (e == a) {
         open = false;
         continue;
       }
       if (!batchable) {
-        job_group[j] = (uint32_t)group_jobs.size();
         group_jobs.push_back({j, j + 1});
         // single-set non-batchable job: CoreVerify (r = 1); multi-set: random linear combination
         for (uint32_t i = a; i < e; i++) scal[i] = (e - a == 1) ? 1ull : splitmix64_at(seed, s0 + i);
@@ -246,113 +301,215 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
         continue;
       }
       for (uint32_t i = a; i < e; i++) scal[i] = splitmix64_at(seed, s0 + i);
-      if (!open || cur_sets >= (uint32_t)ctx->group_sets) {
+      if (!open || cur_sets >= (uint32_t)opt.group_sets) {
         group_jobs.push_back({j, j});
         cur_sets = 0;
         open = true;
       }
-      job_group[j] = (uint32_t)group_jobs.size() - 1;
       group_jobs.back().second = j + 1;
       cur_sets += e - a;
     }
-    hjobs[nj] = n;
   }
   auto job_sets = [&](uint32_t j) {
     const uint32_t gj = sh.job_begin + j;
     return std::make_pair(b.job_first_set[gj] - s0, b.job_first_set[gj + 1] - s0);
   };
+  const uint32_t ng0 = (uint32_t)group_jobs.size();
 
-  // ---- stage inputs in the pinned arena and copy it to the device in one transfer ----------------
-  const uint32_t sstride = b.sig_stride;
+  // ---- message dedupe and same-message units ----------------------------------------------------------------
+  std::vector<uint32_t> msg_idx(n), uniq;
+  if (opt.dedupe) {
+    MsgIndex mi(n, seed ^ 0x6a09e667f3bcc908ull);
+    uniq.reserve(n);
+    for (uint32_t i = 0; i < n; i++) msg_idx[i] = mi.find_or_add(b.msgs + (size_t)s0 * 32, i, uniq);
+  } else {
+    uniq.resize(n);
+    for (uint32_t i = 0; i < n; i++) msg_idx[i] = uniq[i] = i;
+  }
+  const uint32_t n_umsg = (uint32_t)uniq.size();
+  const uint32_t nm = std::max<uint32_t>(n_umsg, 1);
+  // units: within each group, one unit per distinct message
+  std::vector<uint32_t> unit_of_set(n, UINT32_MAX), unit_msg, unit_first, unit_sets, g_unit_first(ng0 + 1, 0);
+  bool merged = false;
+  if (opt.dedupe && n_umsg < n) {
+    std::vector<uint32_t> stamp(n_umsg, UINT32_MAX), unit_of_msg(n_umsg, 0);
+    for (uint32_t g = 0; g < ng0; g++) {
+      g_unit_first[g] = (uint32_t)unit_msg.size();
+      const uint32_t a = job_sets(group_jobs[g].first).first, e = job_sets(group_jobs[g].second - 1).second;
+      for (uint32_t i = a; i < e; i++) {
+        const uint32_t m = msg_idx[i];
+        if (stamp[m] != g) {
+          stamp[m] = g;
+          unit_of_msg[m] = (uint32_t)unit_msg.size();
+          unit_msg.push_back(m);
+        }
+        unit_of_set[i] = unit_of_msg[m];
+      }
+    }
+    g_unit_first[ng0] = (uint32_t)unit_msg.size();
+    merged = unit_msg.size() < (size_t)n;
+    if (merged) {
+      const uint32_t nu = (uint32_t)unit_msg.size();
+      unit_first.assign(nu + 1, 0);
+      for (uint32_t i = 0; i < n; i++)
+        if (unit_of_set[i] != UINT32_MAX) unit_first[unit_of_set[i] + 1]++;
+      for (uint32_t u = 0; u < nu; u++) unit_first[u + 1] += unit_first[u];
+      unit_sets.resize(unit_first[nu]);
+      std::vector<uint32_t> fill(unit_first.begin(), unit_first.end() - 1);
+      for (uint32_t i = 0; i < n; i++)
+        if (unit_of_set[i] != UINT32_MAX) unit_sets[fill[unit_of_set[i]]++] = i;
+    }
+  }
+  const uint32_t n_units = merged ? (uint32_t)unit_msg.size() : 0;
+
+  // ---- stage inputs in the pinned arena and copy it to the device in one transfer ------------------------
+  // arena (256-B aligned sections): scalars | job_first_set | sigs (192 B each) | sig_len | unique msgs |
+  // msg_idx | set ranges | f ranges | units (first, sets, msg) | pk section
+  const size_t o_scal = 0, o_jobs = al256(o_scal + (size_t)n * 8), o_sigs = al256(o_jobs + (size_t)(nj + 1) * 4),
+               o_siglen = al256(o_sigs + (size_t)n * 192), o_umsg = al256(o_siglen + (size_t)n * 4),
+               o_midx = al256(o_umsg + (size_t)n_umsg * 32), o_ranges = al256(o_midx + (size_t)n * 4),
+               o_franges = al256(o_ranges + (size_t)std::max(ng0, 1u) * 8),
+               o_ufirst = al256(o_franges + (size_t)std::max(ng0, 1u) * 8),
+               o_usets = al256(o_ufirst + (size_t)(n_units + 1) * 4), o_umsgi = al256(o_usets + (size_t)unit_sets.size() * 4),
+               o_pk = al256(o_umsgi + (size_t)n_units * 4);
+  size_t in_bytes;
+  if (table_mode)
+    in_bytes = al256(o_pk + (size_t)(n + 1) * 4) + (size_t)npk * 4;
+  else if (bytes_agg)
+    in_bytes = al256(o_pk + (size_t)(n + 1) * 4) + (size_t)npk * 96;
+  else
+    in_bytes = o_pk + (size_t)n * 96;
+  const size_t o_pk2 = al256(o_pk + (size_t)(n + 1) * 4);
+  sl.h_in.ensure(in_bytes);
+  sl.d_in.ensure(in_bytes);
+  uint8_t* const hin = sl.h_in.p;
+  memcpy(hin + o_scal, scal.data(), (size_t)n * 8);
+  uint32_t* hjobs = reinterpret_cast<uint32_t*>(hin + o_jobs);
+  for (uint32_t j = 0; j < nj; j++) hjobs[j] = job_sets(j).first;
+  hjobs[nj] = n;
   uint8_t* hsigs = hin + o_sigs;
   uint32_t* hsiglen = reinterpret_cast<uint32_t*>(hin + o_siglen);
   for (uint32_t i = 0; i < n; i++) {
-    uint32_t len = b.sig_len[s0 + i];
-    uint32_t cl = (len == 96 || len == 192) ? len : 0;
-    memcpy(hsigs + (size_t)i * 192, b.sigs + (size_t)(s0 + i) * sstride, cl);
+    const uint32_t len = b.sig_len[s0 + i];
+    const uint32_t cl = (len == 96 || len == 192) ? len : 0;
+    memcpy(hsigs + (size_t)i * 192, b.sigs + (size_t)(s0 + i) * b.sig_stride, cl);
     hsiglen[i] = len;
   }
-  memcpy(hin + o_msgs, b.msgs + (size_t)s0 * 32, (size_t)n * 32);
-  if (table_mode) {
-    uint32_t* hpkfirst = reinterpret_cast<uint32_t*>(hin + o_pk);
-    const uint32_t base = b.set_pk_first[s0];
-    for (uint32_t i = 0; i <= n; i++) hpkfirst[i] = b.set_pk_first[s0 + i] - base;
-    memcpy(hin + o_pkidx, b.pk_index + base, (size_t)npk * 4);
-  } else {
-    memcpy(hin + o_pk, b.pk_bytes + (size_t)s0 * 96, (size_t)n * 96);
-  }
-  const uint32_t ng0 = (uint32_t)group_jobs.size();
-  const uint32_t max_ranges = std::max<uint32_t>(std::max(ng0, nj), 1);
+  for (uint32_t u = 0; u < n_umsg; u++) memcpy(hin + o_umsg + (size_t)u * 32, b.msgs + (size_t)(s0 + uniq[u]) * 32, 32);
+  memcpy(hin + o_midx, msg_idx.data(), (size_t)n * 4);
   uint32_t* hranges = reinterpret_cast<uint32_t*>(hin + o_ranges);
+  uint32_t* hfranges = reinterpret_cast<uint32_t*>(hin + o_franges);
   for (uint32_t g = 0; g < ng0; g++) {
     hranges[2 * g] = job_sets(group_jobs[g].first).first;
     hranges[2 * g + 1] = job_sets(group_jobs[g].second - 1).second;
+    hfranges[2 * g] = merged ? g_unit_first[g] : hranges[2 * g];
+    hfranges[2 * g + 1] = merged ? g_unit_first[g + 1] : hranges[2 * g + 1];
+  }
+  if (merged) {
+    memcpy(hin + o_ufirst, unit_first.data(), (size_t)(n_units + 1) * 4);
+    memcpy(hin + o_usets, unit_sets.data(), unit_sets.size() * 4);
+    memcpy(hin + o_umsgi, unit_msg.data(), (size_t)n_units * 4);
+  }
+  if (table_mode || bytes_agg) {
+    uint32_t* hpkfirst = reinterpret_cast<uint32_t*>(hin + o_pk);
+    for (uint32_t i = 0; i <= n; i++) hpkfirst[i] = b.set_pk_first[s0 + i] - pk_base;
+    if (table_mode)
+      memcpy(hin + o_pk2, b.pk_index + pk_base, (size_t)npk * 4);
+    else
+      memcpy(hin + o_pk2, b.pk_bytes + (size_t)pk_base * 96, (size_t)npk * 96);
+  } else {
+    memcpy(hin + o_pk, b.pk_bytes + (size_t)s0 * 96, (size_t)n * 96);
   }
 
-  sl.d_flags.ensure((size_t)stride * 2);
-  sl.d_status.ensure((size_t)stride * 2);
-  sl.d_include.ensure(stride);
-  const size_t o_ok = al(nj), res_bytes = o_ok + max_ranges;
+  // byte arrays: flags n | mflags nm | unit_ok n | status 3n | include n ; results: job_err nj | ok ng
+  const size_t ob_flags = 0, ob_mflags = al256(n), ob_unit = al256(ob_mflags + nm), ob_status = al256(ob_unit + n),
+               ob_include = al256(ob_status + 3 * (size_t)stride), bytes_total = al256(ob_include + stride);
+  sl.d_bytes.ensure(bytes_total);
+  const uint32_t max_ranges = std::max<uint32_t>(std::max(ng0, nj), 1);
+  const size_t o_ok = al256(nj), res_bytes = o_ok + max_ranges;
   sl.d_res.ensure(res_bytes);
   sl.h_res.ensure(res_bytes);
   sl.d_S.ensure((size_t)W_G2J * max_ranges);
   sl.d_F.ensure((size_t)W_FP12 * max_ranges);
-  // work area: sig_aff, h_aff, pk_jac, pk_aff, rsig, f
-  const size_t work_words = (size_t)stride * (W_G2A + W_G2A + W_G1J + W_G1A + W_G2J + W_FP12);
-  sl.d_work.ensure(work_words);
-  sl.d_lines.ensure((size_t)stride * kMillerLineWords);
+  // work area: per set sig_aff, pk_jac, pk_aff, rsig, f_set (+ per unit unit_p, f_unit), per message h_aff
+  const size_t per_set = W_G2A + W_G1J + W_G1A + W_G2J + W_FP12 + (merged ? W_G1A + W_FP12 : 0);
+  sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * W_G2A);
+  sl.d_lines.ensure((size_t)nm * kMillerLineWords);
   hipStream_t s = sl.stream;
   uint8_t* const din = sl.d_in.p;
   HIPCHK(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, s));
   uint8_t* const d_ok0 = sl.d_res.p + o_ok;
 
   PipelineBuffers pb;
+  memset(&pb, 0, sizeof pb);
   pb.n = stride;
   pb.sigs = din + o_sigs;
   pb.sig_len = reinterpret_cast<uint32_t*>(din + o_siglen);
   pb.sig_stride = 192;
-  pb.msgs = din + o_msgs;
-  pb.pk_bytes = table_mode ? nullptr : din + o_pk;
-  pb.set_pk_first = table_mode ? reinterpret_cast<uint32_t*>(din + o_pk) : nullptr;
-  pb.pk_index = table_mode ? reinterpret_cast<uint32_t*>(din + o_pkidx) : nullptr;
+  pb.pk_bytes = table_mode ? nullptr : din + (bytes_agg ? o_pk2 : o_pk);
+  pb.set_pk_first = (table_mode || bytes_agg) ? reinterpret_cast<uint32_t*>(din + o_pk) : nullptr;
+  pb.pk_index = table_mode ? reinterpret_cast<uint32_t*>(din + o_pk2) : nullptr;
   pb.pk_table = d.table.p;
   pb.pk_table_n = d.table_n;
   pb.scalars = reinterpret_cast<uint64_t*>(din + o_scal);
   pb.job_first_set = reinterpret_cast<uint32_t*>(din + o_jobs);
   pb.n_jobs = nj;
+  pb.umsgs = din + o_umsg;
+  pb.msg_idx = reinterpret_cast<uint32_t*>(din + o_midx);
+  pb.n_umsg = n_umsg;
+  pb.nm = nm;
+  pb.n_units = n_units;
+  pb.unit_set_first = reinterpret_cast<uint32_t*>(din + o_ufirst);
+  pb.unit_sets = reinterpret_cast<uint32_t*>(din + o_usets);
+  pb.unit_msg = reinterpret_cast<uint32_t*>(din + o_umsgi);
   uint32_t* w = sl.d_work.p;
   pb.sig_aff = w; w += (size_t)stride * W_G2A;
-  pb.h_aff = w; w += (size_t)stride * W_G2A;
   pb.pk_jac = w; w += (size_t)stride * W_G1J;
   pb.pk_aff = w; w += (size_t)stride * W_G1A;
   pb.rsig = w; w += (size_t)stride * W_G2J;
-  pb.f = w;
+  pb.f_set = w; w += (size_t)stride * W_FP12;
+  if (merged) {
+    pb.unit_p = w; w += (size_t)stride * W_G1A;
+    pb.f_unit = w; w += (size_t)stride * W_FP12;
+  }
+  pb.h_aff = w;
   pb.lines = sl.d_lines.p;
-  pb.flags = sl.d_flags.p;
-  pb.status = sl.d_status.p;
+  uint8_t* const db = sl.d_bytes.p;
+  pb.flags = db + ob_flags;
+  pb.mflags = db + ob_mflags;
+  pb.unit_ok = db + ob_unit;
+  pb.status = reinterpret_cast<int8_t*>(db + ob_status);
+  pb.include = db + ob_include;
   pb.job_err = reinterpret_cast<int8_t*>(sl.d_res.p);
-  pb.include = sl.d_include.p;
 
-  // ---- kernel pipeline ---------------------------------------------------------------------------
-  const bool prof = ctx->profile;
+  // ---- kernel pipeline ------------------------------------------------------------------------------------
+  const bool prof = opt.profile;
   auto mark = [&](int k) {
     if (prof) HIPCHK(hipEventRecord(sl.ev[k], s));
   };
   mark(0);
   launch_sig_decode(pb, n, s);
   mark(1);
-  launch_hash_to_g2(pb, n, s);
+  launch_hash_to_g2(pb, s);
   mark(2);
-  if (table_mode) launch_pk_aggregate(pb, n, s);
+  if (table_mode || bytes_agg) launch_pk_aggregate(pb, n, s);
   mark(3);
   launch_pk_finish(pb, n, s);
   mark(4);
   launch_sig_scale(pb, n, s);
-  mark(5);
-  launch_miller_sets(pb, n, s);
   launch_job_mask(pb, s);
+  mark(5);
+  launch_miller_lines(pb, s);
+  if (merged) {
+    launch_unit_aggregate(pb, s);
+    launch_miller_acc(pb, true, n_units, nullptr, s);
+  } else {
+    launch_miller_acc(pb, false, n, nullptr, s);
+  }
   mark(6);
-  launch_group_reduce(pb, reinterpret_cast<uint32_t*>(din + o_ranges), ng0, sl.d_S.p, sl.d_F.p, s);
+  const uint32_t* d_ranges = reinterpret_cast<uint32_t*>(din + o_ranges);
+  const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
+  launch_group_reduce(pb, d_ranges, d_franges, !merged, ng0, sl.d_S.p, sl.d_F.p, s);
   mark(7);
   launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, s);
   mark(8);
@@ -360,6 +517,8 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
   HIPCHK(hipMemcpyAsync(sl.h_res.p, sl.d_res.p, o_ok + ng0, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   st.groups += ng0;
+  st.unique_messages += n_umsg;
+  st.pairing_units += merged ? n_units : n;
   if (prof) {
     for (int k = 0; k < kStages; k++) {
       float ms = 0;
@@ -368,14 +527,13 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
     }
   }
 
-  // ---- per-job results ---------------------------------------------------------------------------
+  // ---- per-job results -------------------------------------------------------------------------------------
   std::vector<int> jr(nj, 0);
   for (uint32_t j = 0; j < nj; j++) {
     const int err = (int8_t)sl.h_res.p[j];
     jr[j] = err ? -err : 2;  // 2 = pending
   }
-  // pending work: lists of clean jobs whose batch equation failed
-  std::vector<std::vector<uint32_t>> failed;
+  std::vector<uint32_t> retry;  // clean jobs of failed groups, each re-checked on its own
   for (uint32_t g = 0; g < ng0; g++) {
     std::vector<uint32_t> clean;
     for (uint32_t j = group_jobs[g].first; j < group_jobs[g].second; j++)
@@ -385,62 +543,60 @@ int run_shard(blsgpu_ctx* ctx, Device& d, Slot& sl, const blsgpu_batch& b, const
       for (uint32_t j : clean) jr[j] = 1;
       if (group_jobs[g].second - group_jobs[g].first > 1)
         for (uint32_t j : clean) st.batch_sigs_success += job_sets(j).second - job_sets(j).first;
-    } else if (clean.size() == 1) {
+    } else if (clean.size() == 1) {  // the group's equation was this job's own
       jr[clean[0]] = 0;
     } else {
-      st.batch_retries++;
-      failed.push_back(std::move(clean));
+      if (clean.size() > 1) st.batch_retries++;
+      retry.insert(retry.end(), clean.begin(), clean.end());
     }
   }
 
-  // ---- fallback: k-ary bisection of failed groups -------------------------------------------------
-  while (!failed.empty()) {
-    std::vector<std::vector<uint32_t>> parts;
-    for (auto& jobs : failed) {
-      const size_t k = std::min<size_t>(split_ways, jobs.size());
-      for (size_t p = 0; p < k; p++) {
-        size_t lo = jobs.size() * p / k, hi = jobs.size() * (p + 1) / k;
-        if (hi > lo) parts.emplace_back(jobs.begin() + lo, jobs.begin() + hi);
-      }
+  // ---- fallback: one parallel launch re-checks every clean job of every failed group -----------------------
+  if (!retry.empty()) {
+    const uint32_t nr = (uint32_t)retry.size();
+    uint32_t n_list = 0;
+    if (merged) {  // per-set Miller values of the retried jobs' sets (units only exist per group)
+      for (uint32_t j : retry) n_list += job_sets(j).second - job_sets(j).first;
     }
-    const uint32_t np = (uint32_t)parts.size();
-    sl.h_ranges.ensure(2 * np);
-    sl.d_ranges.ensure(2 * np);
-    sl.d_ok.ensure(np);
-    sl.h_ok.ensure(np);
-    sl.d_S.ensure((size_t)W_G2J * np);
-    sl.d_F.ensure((size_t)W_FP12 * np);
-    for (uint32_t q = 0; q < np; q++) {
-      sl.h_ranges.p[2 * q] = job_sets(parts[q].front()).first;
-      sl.h_ranges.p[2 * q + 1] = job_sets(parts[q].back()).second;
+    sl.h_list.ensure(2 * (size_t)nr + n_list);
+    sl.d_list.ensure(2 * (size_t)nr + n_list);
+    uint32_t* hl = sl.h_list.p;
+    for (uint32_t q = 0; q < nr; q++) {
+      hl[2 * q] = job_sets(retry[q]).first;
+      hl[2 * q + 1] = job_sets(retry[q]).second;
     }
-    // Sub-ranges may span error jobs between clean ones; their sets are masked out on the device.  A
-    // single-job part covers exactly its own sets, so every final `false` is decided on the job alone.
-    HIPCHK(hipMemcpyAsync(sl.d_ranges.p, sl.h_ranges.p, (size_t)np * 8, hipMemcpyHostToDevice, s));
-    launch_group_reduce(pb, sl.d_ranges.p, np, sl.d_S.p, sl.d_F.p, s);
-    launch_group_check(sl.d_S.p, sl.d_F.p, np, sl.d_ok.p, s);
+    uint32_t* sets_list = hl + 2 * (size_t)nr;
+    uint32_t k = 0;
+    if (merged)
+      for (uint32_t j : retry)
+        for (uint32_t i = job_sets(j).first; i < job_sets(j).second; i++) sets_list[k++] = i;
+    sl.d_ok.ensure(nr);
+    sl.h_ok.ensure(nr);
+    sl.d_S.ensure((size_t)W_G2J * nr);
+    sl.d_F.ensure((size_t)W_FP12 * nr);
+    HIPCHK(hipMemcpyAsync(sl.d_list.p, hl, (2 * (size_t)nr + n_list) * 4, hipMemcpyHostToDevice, s));
+    if (merged) launch_miller_acc(pb, false, n_list, sl.d_list.p + 2 * (size_t)nr, s);
+    launch_group_reduce(pb, sl.d_list.p, sl.d_list.p, true, nr, sl.d_S.p, sl.d_F.p, s);
+    launch_group_check(sl.d_S.p, sl.d_F.p, nr, sl.d_ok.p, s);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, np, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, nr, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    std::vector<std::vector<uint32_t>> next;
-    for (uint32_t q = 0; q < np; q++) {
-      if (sl.h_ok.p[q]) {
-        for (uint32_t j : parts[q]) jr[j] = 1;
-      } else if (parts[q].size() == 1) {
-        jr[parts[q][0]] = 0;
-      } else {
-        next.push_back(std::move(parts[q]));
-      }
-    }
-    failed.swap(next);
+    for (uint32_t q = 0; q < nr; q++) jr[retry[q]] = sl.h_ok.p[q] ? 1 : 0;
   }
   for (uint32_t j = 0; j < nj; j++) job_result[sh.job_begin + j] = (int8_t)jr[j];
   return BLSGPU_OK;
 }
 
-int validate_batch(const blsgpu_ctx* ctx, const blsgpu_batch* b) {
+uint32_t max_table_index(const blsgpu_batch* b) {
+  uint32_t m = 0;
+  if (!b->pk_bytes && b->n_sets)
+    for (uint32_t k = 0; k < b->set_pk_first[b->n_sets]; k++) m = std::max(m, b->pk_index[k]);
+  return m;
+}
+
+int validate_batch(const blsgpu_batch* b) {
   if (!b || !b->job_first_set) return BLSGPU_ERR_ARGS;
-  if (b->n_jobs == 0) return BLSGPU_OK;
+  if (b->n_jobs == 0) return b->n_sets == 0 ? BLSGPU_OK : BLSGPU_ERR_ARGS;
   if (b->job_first_set[0] != 0 || b->job_first_set[b->n_jobs] != b->n_sets) return BLSGPU_ERR_ARGS;
   for (uint32_t j = 0; j < b->n_jobs; j++)
     if (b->job_first_set[j + 1] < b->job_first_set[j]) return BLSGPU_ERR_ARGS;
@@ -449,16 +605,161 @@ int validate_batch(const blsgpu_ctx* ctx, const blsgpu_batch* b) {
   if (b->sig_stride < 96) return BLSGPU_ERR_ARGS;
   for (uint32_t i = 0; i < b->n_sets; i++)
     if (b->sig_len[i] > b->sig_stride && (b->sig_len[i] == 96 || b->sig_len[i] == 192)) return BLSGPU_ERR_ARGS;
-  if (!b->pk_bytes) {
-    if (!b->set_pk_first || !b->pk_index) return BLSGPU_ERR_ARGS;
+  if (!b->pk_bytes && (!b->set_pk_first || !b->pk_index)) return BLSGPU_ERR_ARGS;
+  if (b->set_pk_first) {
     if (b->set_pk_first[0] != 0) return BLSGPU_ERR_ARGS;
     for (uint32_t i = 0; i < b->n_sets; i++)
       if (b->set_pk_first[i + 1] < b->set_pk_first[i]) return BLSGPU_ERR_ARGS;
-    uint32_t tn = ctx->devs.empty() ? 0 : ctx->devs[0]->table_n;
-    for (uint32_t k = 0; k < b->set_pk_first[b->n_sets]; k++)
-      if (b->pk_index[k] >= tn) return BLSGPU_ERR_ARGS;
   }
   return BLSGPU_OK;
+}
+
+bool enter(blsgpu_ctx* ctx) {  // register a call in progress unless the context is closing
+  std::lock_guard<std::mutex> lk(ctx->active_mu);
+  if (ctx->closed) return false;
+  ctx->active++;
+  return true;
+}
+void leave(blsgpu_ctx* ctx) {
+  {
+    std::lock_guard<std::mutex> lk(ctx->active_mu);
+    ctx->active--;
+  }
+  ctx->active_cv.notify_all();
+}
+
+void finish_call(Call* c) {
+  blsgpu_stats local{};
+  int status = BLSGPU_OK;
+  for (int k = 0; k < kStages; k++) local.stage_ms[k] = c->sst.empty() ? 0 : c->sst[0].stage_ms[k];
+  for (size_t k = 0; k < c->shards.size(); k++) {
+    local.groups += c->sst[k].groups;
+    local.batch_retries += c->sst[k].batch_retries;
+    local.batch_sigs_success += c->sst[k].batch_sigs_success;
+    local.unique_messages += c->sst[k].unique_messages;
+    local.pairing_units += c->sst[k].pairing_units;
+    if (c->rc[k] != BLSGPU_OK && c->rc[k] != BLSGPU_DEVICE_ERROR) status = c->rc[k];
+  }
+  local.devices_used = (uint32_t)c->shards.size();
+  local.device_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->t0).count();
+  if (c->stats) *c->stats = local;
+  blsgpu_ctx* ctx = c->ctx;
+  if (c->sync) {
+    // notify under the lock: the waiter may destroy *c as soon as it can re-acquire it
+    std::lock_guard<std::mutex> lk(c->m);
+    c->status = status;
+    c->finished = true;
+    c->cv.notify_all();
+  } else {
+    blsgpu_done_cb done = c->done;
+    void* user = c->user;
+    delete c->owned;
+    delete c;
+    if (done) done(user, status);
+  }
+  leave(ctx);
+}
+
+void run_task(Device& d, Slot& sl, const Task& t) {
+  Call* c = t.call;
+  const Shard& sh = c->shards[t.shard];
+  int rc;
+  if (c->ctx->closed && !c->sync) {
+    rc = BLSGPU_ERR_CLOSED;
+  } else {
+    try {
+      std::shared_lock<std::shared_mutex> tl(d.table_mu);
+      rc = run_shard(d, sl, c->b, sh, c->job_result, c->seed, c->opt, c->max_index, c->sst[t.shard]);
+    } catch (...) {
+      rc = BLSGPU_DEVICE_ERROR;
+    }
+  }
+  if (rc == BLSGPU_DEVICE_ERROR)  // a device failure rejects every job of the shard, never `false`
+    for (uint32_t j = sh.job_begin; j < sh.job_end; j++) c->job_result[j] = -BLSGPU_DEVICE_ERROR;
+  c->rc[t.shard] = rc;
+  if (c->remaining.fetch_sub(1) == 1) finish_call(c);
+}
+
+void worker_loop(Device* d, Slot* sl) {
+  (void)hipSetDevice(d->id);
+  for (;;) {
+    Task t;
+    {
+      std::unique_lock<std::mutex> lk(d->q_mu);
+      d->q_cv.wait(lk, [&] { return d->stop || !d->queue.empty(); });
+      if (d->queue.empty()) return;  // stop requested and nothing left
+      t = d->queue.front();
+      d->queue.pop_front();
+    }
+    run_task(*d, *sl, t);
+  }
+}
+
+void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet shared)
+  Slot* s = new Slot();
+  HIPCHK(hipSetDevice(d->id));
+  HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
+  d->slots.push_back(s);
+  d->workers.emplace_back(worker_loop, d, s);
+}
+
+void destroy_device(Device* d) {
+  {
+    std::lock_guard<std::mutex> lk(d->q_mu);
+    d->stop = true;
+  }
+  d->q_cv.notify_all();
+  for (auto& t : d->workers) t.join();
+  (void)hipSetDevice(d->id);
+  for (Slot* s : d->slots) {
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    s->release_all();
+    for (auto& e : s->ev)
+      if (e) (void)hipEventDestroy(e);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+  }
+  d->helper.release_all();
+  d->table.release();
+  if (d->table_stream) (void)hipStreamDestroy(d->table_stream);
+  delete d;
+}
+
+// Shards a call over the devices and queues the shard tasks.
+void launch_call(blsgpu_ctx* ctx, Call* c) {
+  const blsgpu_batch& b = c->b;
+  const uint32_t nd_all = (uint32_t)std::min<int64_t>((int64_t)ctx->devs.size(), c->opt.max_devices);
+  const uint32_t nd = std::max<uint32_t>(1, std::min<uint32_t>(nd_all, (b.n_sets + 255) / 256));
+  std::vector<uint32_t> parts(nd + 1);
+  shard_rule(b.job_first_set, b.set_pk_first, b.n_jobs, nd, parts.data());
+  for (uint32_t k = 0; k < nd; k++)
+    c->shards.push_back({parts[k], parts[k + 1], b.n_jobs ? b.job_first_set[parts[k]] : 0,
+                         b.n_jobs ? b.job_first_set[parts[k + 1]] : 0});
+  c->sst.assign(nd, blsgpu_stats{});
+  c->rc.assign(nd, BLSGPU_OK);
+  c->remaining = nd;
+  c->t0 = std::chrono::steady_clock::now();
+  for (uint32_t k = 0; k < nd; k++) {
+    Device* d = ctx->devs[k];
+    {
+      std::lock_guard<std::mutex> lk(d->q_mu);
+      d->queue.push_back({c, k});
+    }
+    d->q_cv.notify_one();
+  }
+}
+
+uint64_t resolve_seed(uint64_t seed) {
+  while (seed == 0) {
+    if (getrandom(&seed, sizeof(seed), 0) != (ssize_t)sizeof(seed)) seed = 0x4C4F444553544152ull;
+  }
+  return seed;
+}
+
+Options snapshot(blsgpu_ctx* ctx) {
+  std::lock_guard<std::mutex> lk(ctx->opt_mu);
+  return ctx->opt;
 }
 
 }  // namespace
@@ -468,17 +769,9 @@ extern "C" {
 int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
   if (!out) return BLSGPU_ERR_ARGS;
   *out = nullptr;
-  // Slots need hardware queues of their own: kernels of streams that share one run in order, so a batch's
-  // long single-batch tail (k_group_check) blocks the next batch's stage kernels.  HIP's default (and the
-  // usual environment) is 4 queues per process; on MI355X 8 measured 1.70M vs 1.32M sets/s on C2 with 12
-  // slots, and 16 fails queue creation (HSA_STATUS_ERROR_OUT_OF_RESOURCES) -- profiles/r01_hwq.json.  So a
-  // setting below 8 is raised to 8 (BLSGPU_KEEP_HW_QUEUES=1 keeps it).  HIP reads it once, at its
-  // initialization, so this only takes effect when blsgpu_init is the process's first HIP call.
-  {
-    const char* q = getenv("GPU_MAX_HW_QUEUES");
-    const char* keep = getenv("BLSGPU_KEEP_HW_QUEUES");
-    if (!(keep && keep[0] == '1') && (!q || atoi(q) < 8)) setenv("GPU_MAX_HW_QUEUES", "8", 1);
-  }
+  // Concurrent calls use one slot (and HIP stream) each; streams that share an in-order hardware queue
+  // serialize.  HIP reads GPU_MAX_HW_QUEUES once, at its initialization: the launcher sets it (bench.py and
+  // the Node addon's loader set 8 before the first HIP call; DESIGN.md "Hardware queues").
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return BLSGPU_ERR_NO_DEVICE;
   std::vector<int> ids;
@@ -498,7 +791,7 @@ int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
       ctx->devs.push_back(d);
       HIPCHK(hipSetDevice(id));
       HIPCHK(hipStreamCreateWithFlags(&d->table_stream, hipStreamNonBlocking));
-      for (int k = 0; k < 4; k++) d->add_slot();
+      for (int k = 0; k < ctx->slots_per_device; k++) add_slot(d);
     }
   } catch (HipError&) {
     blsgpu_destroy(ctx);
@@ -510,39 +803,41 @@ int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
 
 void blsgpu_destroy(blsgpu_ctx* ctx) {
   if (!ctx) return;
-  ctx->closed = true;
   {
-    std::unique_lock<std::mutex> lk(ctx->async_mu);
-    ctx->async_cv.wait(lk, [&] { return ctx->inflight.load() == 0; });
+    std::unique_lock<std::mutex> lk(ctx->active_mu);
+    ctx->closed = true;  // queued asynchronous shards now complete with BLSGPU_ERR_CLOSED
+    ctx->active_cv.wait(lk, [&] { return ctx->active == 0; });
   }
-  for (Device* d : ctx->devs) {
-    // wait until no synchronous caller holds a slot
-    {
-      std::unique_lock<std::mutex> lk(d->slot_mu);
-      d->slot_cv.wait(lk, [&] { return d->free_slots.size() == d->slots.size(); });
-    }
-    d->destroy_all();
-    delete d;
-  }
+  for (Device* d : ctx->devs) destroy_device(d);
   delete ctx;
 }
 
 int blsgpu_device_count(const blsgpu_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
 
 uint32_t blsgpu_pubkeys_count(const blsgpu_ctx* ctx) {
-  return (ctx && !ctx->devs.empty()) ? ctx->devs[0]->table_n : 0;
+  if (!ctx || ctx->devs.empty()) return 0;
+  uint32_t n = UINT32_MAX;
+  for (Device* d : ctx->devs) {
+    std::shared_lock<std::shared_mutex> lk(d->table_mu);
+    n = std::min(n, d->table_n);
+  }
+  return n;
 }
 
 int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* pk96, uint32_t n) {
   if (!ctx) return BLSGPU_ERR_ARGS;
-  if (ctx->closed) return BLSGPU_ERR_CLOSED;
   if (n == 0) return BLSGPU_OK;
   if (!pk96) return BLSGPU_ERR_ARGS;
+  if (!enter(ctx)) return BLSGPU_ERR_CLOSED;
   std::lock_guard<std::mutex> tl(ctx->table_mu);
   int result = BLSGPU_OK;
+  for (Device* d : ctx->devs) {  // no gaps: an upload may only extend or overwrite the table
+    std::shared_lock<std::shared_mutex> lk(d->table_mu);
+    if (first_index > d->table_n) result = BLSGPU_ERR_ARGS;
+  }
   try {
     for (Device* d : ctx->devs) {
-      std::unique_lock<std::shared_mutex> lk(d->table_mu);
+      if (result) break;
       HIPCHK(hipSetDevice(d->id));
       hipStream_t ts = d->table_stream;
       const uint32_t need = first_index + n;
@@ -561,6 +856,7 @@ int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* 
       int err = 0;
       for (uint32_t i = 0; i < n && !err; i++) err = hst[i];
       if (!err) {
+        std::unique_lock<std::shared_mutex> lk(d->table_mu);
         if (need > d->table.cap / W_PKTAB) {
           DevBuf<uint32_t> nt;
           nt.ensure((size_t)std::max<uint32_t>(need, d->table_n + d->table_n / 2) * W_PKTAB);
@@ -576,42 +872,43 @@ int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* 
       (void)hipFree(dpk);
       (void)hipFree(dst);
       (void)hipFree(tmp);
-      if (err) {
-        result = err;
-        break;
-      }
+      if (err) result = err;
     }
   } catch (HipError&) {
-    return BLSGPU_DEVICE_ERROR;
+    result = BLSGPU_DEVICE_ERROR;
   }
+  leave(ctx);
   return result;
 }
 
 int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return BLSGPU_ERR_ARGS;
   std::string k(key);
-  std::lock_guard<std::mutex> lk(ctx->opt_mu);
-  if (k == "group_sets") {
-    if (value < 1) return BLSGPU_ERR_ARGS;
-    ctx->group_sets = value;
-  } else if (k == "profile") {
-    ctx->profile = value != 0;
-  } else if (k == "max_devices") {
-    if (value < 1) return BLSGPU_ERR_ARGS;
-    ctx->max_devices = value;
-  } else if (k == "split_ways") {
-    if (value < 2) return BLSGPU_ERR_ARGS;
-    ctx->split_ways = value;
-  } else if (k == "slots") {
+  if (k == "slots") {
     if (value < 1 || value > 64) return BLSGPU_ERR_ARGS;
     try {
       for (Device* d : ctx->devs) {
-        std::lock_guard<std::mutex> sl(d->slot_mu);
-        while ((int64_t)d->slots.size() < value) d->add_slot();
+        std::lock_guard<std::mutex> lk(d->q_mu);
+        while ((int64_t)d->slots.size() < value) add_slot(d);
       }
     } catch (HipError&) {
       return BLSGPU_DEVICE_ERROR;
     }
+    std::lock_guard<std::mutex> lk(ctx->opt_mu);
+    ctx->slots_per_device = std::max<int64_t>(ctx->slots_per_device, value);
+    return BLSGPU_OK;
+  }
+  std::lock_guard<std::mutex> lk(ctx->opt_mu);
+  if (k == "group_sets") {
+    if (value < 1) return BLSGPU_ERR_ARGS;
+    ctx->opt.group_sets = value;
+  } else if (k == "profile") {
+    ctx->opt.profile = value != 0;
+  } else if (k == "max_devices") {
+    if (value < 1) return BLSGPU_ERR_ARGS;
+    ctx->opt.max_devices = value;
+  } else if (k == "dedupe") {
+    ctx->opt.dedupe = value != 0;
   } else {
     return BLSGPU_ERR_ARGS;
   }
@@ -620,131 +917,87 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
 
 int blsgpu_verify(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, blsgpu_stats* stats) {
   if (!ctx) return BLSGPU_ERR_ARGS;
-  if (ctx->closed) return BLSGPU_ERR_CLOSED;
-  int v = validate_batch(ctx, b);
+  int v = validate_batch(b);
   if (v) return v;
   if (b->n_jobs && !job_result) return BLSGPU_ERR_ARGS;
-  blsgpu_stats local{};
-  uint64_t seed = b->seed;
-  if (seed == 0) {
-    while (seed == 0) {
-      if (getrandom(&seed, sizeof(seed), 0) != (ssize_t)sizeof(seed)) return BLSGPU_ERR_ARGS;
-    }
+  if (!enter(ctx)) return BLSGPU_ERR_CLOSED;
+  Call c;
+  c.ctx = ctx;
+  c.b = *b;
+  c.job_result = job_result;
+  c.stats = stats;
+  c.seed = resolve_seed(b->seed);
+  c.max_index = max_table_index(b);
+  c.opt = snapshot(ctx);
+  c.sync = true;
+  if (b->n_jobs == 0) {
+    if (stats) *stats = blsgpu_stats{};
+    leave(ctx);
+    return BLSGPU_OK;
   }
-  // cost-balanced contiguous sharding of jobs over devices
-  const uint32_t nd_all = (uint32_t)std::min<int64_t>((int64_t)ctx->devs.size(), ctx->max_devices);
-  const uint32_t nd = std::max<uint32_t>(1, std::min<uint32_t>(nd_all, (b->n_sets + 255) / 256));
-  std::vector<double> cost(b->n_jobs + 1, 0.0);
-  for (uint32_t j = 0; j < b->n_jobs; j++) {
-    double c = 0;
-    for (uint32_t i = b->job_first_set[j]; i < b->job_first_set[j + 1]; i++) {
-      c += 1.0;
-      if (!b->pk_bytes) c += (b->set_pk_first[i + 1] - b->set_pk_first[i]) / 256.0;
-    }
-    cost[j + 1] = cost[j] + c;
-  }
-  std::vector<Shard> shards;
-  uint32_t j0 = 0;
-  for (uint32_t k = 0; k < nd; k++) {
-    double target = cost[b->n_jobs] * (k + 1) / nd;
-    uint32_t j1 = j0;
-    if (k + 1 == nd) {
-      j1 = b->n_jobs;
-    } else {
-      while (j1 < b->n_jobs && cost[j1 + 1] <= target) j1++;
-    }
-    shards.push_back({j0, j1, b->job_first_set[j0], b->job_first_set[j1]});
-    j0 = j1;
-  }
-  auto t0 = std::chrono::steady_clock::now();
-  std::vector<blsgpu_stats> sst(shards.size());
-  std::vector<int> rc(shards.size(), BLSGPU_OK);
-  auto work = [&](size_t k) {
-    Device& d = *ctx->devs[k];
-    std::shared_lock<std::shared_mutex> tl(d.table_mu);
-    Slot* sl = d.acquire();
-    try {
-      rc[k] = run_shard(ctx, d, *sl, *b, shards[k], job_result, seed, sst[k]);
-    } catch (HipError&) {
-      rc[k] = BLSGPU_DEVICE_ERROR;
-    } catch (...) {
-      rc[k] = BLSGPU_DEVICE_ERROR;
-    }
-    d.release(sl);
-    if (rc[k] == BLSGPU_DEVICE_ERROR)
-      for (uint32_t j = shards[k].job_begin; j < shards[k].job_end; j++) job_result[j] = -BLSGPU_DEVICE_ERROR;
-  };
-  if (shards.size() == 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> th;
-    for (size_t k = 0; k < shards.size(); k++) th.emplace_back(work, k);
-    for (auto& t : th) t.join();
-  }
-  auto t1 = std::chrono::steady_clock::now();
-  int status = BLSGPU_OK;
-  for (int k = 0; k < kStages; k++) local.stage_ms[k] = sst[0].stage_ms[k];
-  for (size_t k = 0; k < shards.size(); k++) {
-    local.groups += sst[k].groups;
-    local.batch_retries += sst[k].batch_retries;
-    local.batch_sigs_success += sst[k].batch_sigs_success;
-    if (rc[k] != BLSGPU_OK) status = rc[k];
-  }
-  local.devices_used = (uint32_t)shards.size();
-  local.device_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-  if (stats) *stats = local;
-  return status == BLSGPU_DEVICE_ERROR ? BLSGPU_OK : status;  // device errors are reported per job
+  launch_call(ctx, &c);
+  std::unique_lock<std::mutex> lk(c.m);
+  c.cv.wait(lk, [&] { return c.finished; });
+  return c.status;  // device errors are reported per job
 }
 
 int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, blsgpu_stats* stats,
                   blsgpu_done_cb done, void* user) {
   if (!ctx || !b) return BLSGPU_ERR_ARGS;
-  if (ctx->closed) return BLSGPU_ERR_CLOSED;
-  int v = validate_batch(ctx, b);
+  int v = validate_batch(b);
   if (v) return v;
+  if (b->n_jobs && !job_result) return BLSGPU_ERR_ARGS;
+  if (!enter(ctx)) return BLSGPU_ERR_CLOSED;
   // deep-copy the inputs so the caller may reuse its buffers immediately
-  struct Owned {
-    blsgpu_batch b;
-    std::vector<uint32_t> jfs, siglen, pkfirst, pkidx;
-    std::vector<uint8_t> jflags, pkb, msgs, sigs;
-  };
+  Call* c = new Call();
   Owned* o = new Owned();
-  o->b = *b;
+  c->ctx = ctx;
+  c->owned = o;
+  c->b = *b;
   o->jfs.assign(b->job_first_set, b->job_first_set + b->n_jobs + 1);
-  o->b.job_first_set = o->jfs.data();
+  c->b.job_first_set = o->jfs.data();
   if (b->job_flags) {
     o->jflags.assign(b->job_flags, b->job_flags + b->n_jobs);
-    o->b.job_flags = o->jflags.data();
+    c->b.job_flags = o->jflags.data();
   }
   o->siglen.assign(b->sig_len, b->sig_len + b->n_sets);
-  o->b.sig_len = o->siglen.data();
+  c->b.sig_len = o->siglen.data();
   o->sigs.assign(b->sigs, b->sigs + (size_t)b->n_sets * b->sig_stride);
-  o->b.sigs = o->sigs.data();
+  c->b.sigs = o->sigs.data();
   o->msgs.assign(b->msgs, b->msgs + (size_t)b->n_sets * 32);
-  o->b.msgs = o->msgs.data();
-  if (b->pk_bytes) {
-    o->pkb.assign(b->pk_bytes, b->pk_bytes + (size_t)b->n_sets * 96);
-    o->b.pk_bytes = o->pkb.data();
-  } else {
+  c->b.msgs = o->msgs.data();
+  const uint32_t npk = b->set_pk_first ? b->set_pk_first[b->n_sets] : b->n_sets;
+  if (b->set_pk_first) {
     o->pkfirst.assign(b->set_pk_first, b->set_pk_first + b->n_sets + 1);
-    o->pkidx.assign(b->pk_index, b->pk_index + b->set_pk_first[b->n_sets]);
-    o->b.set_pk_first = o->pkfirst.data();
-    o->b.pk_index = o->pkidx.data();
+    c->b.set_pk_first = o->pkfirst.data();
   }
-  {
-    std::lock_guard<std::mutex> lk(ctx->async_mu);
-    ctx->inflight++;
+  if (b->pk_bytes) {
+    o->pkb.assign(b->pk_bytes, b->pk_bytes + (size_t)npk * 96);
+    c->b.pk_bytes = o->pkb.data();
+  } else {
+    o->pkidx.assign(b->pk_index, b->pk_index + npk);
+    c->b.pk_index = o->pkidx.data();
   }
-  std::thread([ctx, o, job_result, stats, done, user]() {
-    int rc = ctx->closed ? BLSGPU_ERR_CLOSED : blsgpu_verify(ctx, &o->b, job_result, stats);
-    delete o;
-    if (done) done(user, rc);
-    {
-      std::lock_guard<std::mutex> lk(ctx->async_mu);
-      ctx->inflight--;
-    }
-    ctx->async_cv.notify_all();
-  }).detach();
+  c->job_result = job_result;
+  c->stats = stats;
+  c->seed = resolve_seed(b->seed);
+  c->max_index = max_table_index(&c->b);
+  c->opt = snapshot(ctx);
+  c->done = done;
+  c->user = user;
+  if (b->n_jobs == 0) {
+    c->shards.clear();
+    finish_call(c);  // calls done(user, OK) and leaves
+    return BLSGPU_OK;
+  }
+  launch_call(ctx, c);
+  return BLSGPU_OK;
+}
+
+int blsgpu_shard_jobs(const uint32_t* job_first_set, const uint32_t* set_pk_first, uint32_t n_jobs,
+                      uint32_t n_parts, uint32_t* part_first_job) {
+  if (!job_first_set || !part_first_job || n_parts == 0) return BLSGPU_ERR_ARGS;
+  shard_rule(job_first_set, set_pk_first, n_jobs, n_parts, part_first_job);
   return BLSGPU_OK;
 }
 
@@ -769,34 +1022,154 @@ const char* blsgpu_code_name(int code) {
   }
 }
 
+// ---- synchronous helpers on device 0's helper stream ----------------------------------------------------------
+int blsgpu_aggregate_pubkeys(blsgpu_ctx* ctx, const blsgpu_batch* b, uint8_t* out, uint32_t out_len,
+                             int8_t* status) {
+  if (!ctx || ctx->devs.empty() || !b || !out || !status || (out_len != 48 && out_len != 96)) return BLSGPU_ERR_ARGS;
+  const uint32_t n = b->n_sets;
+  if (n == 0) return BLSGPU_OK;
+  if (!b->pk_bytes && (!b->set_pk_first || !b->pk_index)) return BLSGPU_ERR_ARGS;
+  if (!enter(ctx)) return BLSGPU_ERR_CLOSED;
+  Device* d = ctx->devs[0];
+  int rc = BLSGPU_OK;
+  try {
+    std::lock_guard<std::mutex> hl(d->helper_mu);
+    std::shared_lock<std::shared_mutex> tl(d->table_mu);
+    HIPCHK(hipSetDevice(d->id));
+    // set_pk_first (a synthetic 1-key-per-set layout in single-key bytes mode) | keys | out | status
+    std::vector<uint32_t> spf(n + 1);
+    for (uint32_t i = 0; i <= n; i++) spf[i] = b->set_pk_first ? b->set_pk_first[i] : i;
+    const uint32_t npk = spf[n];
+    if (!b->pk_bytes) {
+      for (uint32_t k = 0; k < npk; k++)
+        if (b->pk_index[k] >= d->table_n) rc = BLSGPU_ERR_ARGS;
+    }
+    if (rc == BLSGPU_OK) {
+      const size_t key_bytes = b->pk_bytes ? (size_t)npk * 96 : (size_t)npk * 4;
+      const size_t o_keys = al256((size_t)(n + 1) * 4), o_out = al256(o_keys + key_bytes),
+                   o_st = al256(o_out + (size_t)n * out_len), total = o_st + 3 * (size_t)n;
+      Slot& sl = d->helper;
+      sl.d_in.ensure(total);
+      sl.d_work.ensure((size_t)n * W_G1J);
+      hipStream_t s = d->table_stream;
+      uint8_t* din = sl.d_in.p;
+      HIPCHK(hipMemcpyAsync(din, spf.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(din + o_keys, b->pk_bytes ? (const void*)b->pk_bytes : (const void*)b->pk_index,
+                            key_bytes, hipMemcpyHostToDevice, s));
+      PipelineBuffers pb;
+      memset(&pb, 0, sizeof pb);
+      pb.n = n;
+      pb.set_pk_first = reinterpret_cast<uint32_t*>(din);
+      pb.pk_bytes = b->pk_bytes ? din + o_keys : nullptr;
+      pb.pk_index = b->pk_bytes ? nullptr : reinterpret_cast<uint32_t*>(din + o_keys);
+      pb.pk_table = d->table.p;
+      pb.pk_table_n = d->table_n;
+      pb.pk_jac = sl.d_work.p;
+      pb.status = reinterpret_cast<int8_t*>(din + o_st);
+      launch_pk_aggregate(pb, n, s);
+      launch_pk_serialize(pb, n, din + o_out, out_len, s);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(out, din + o_out, (size_t)n * out_len, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(status, din + o_st, n, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+  } catch (HipError&) {
+    rc = BLSGPU_DEVICE_ERROR;
+  }
+  leave(ctx);
+  return rc;
+}
+
+int blsgpu_key_validate(blsgpu_ctx* ctx, uint32_t n, const uint8_t* pks, uint32_t pk_len, uint32_t stride,
+                        uint8_t* out96, int8_t* status) {
+  if (!ctx || ctx->devs.empty() || !pks || !status || stride < pk_len) return BLSGPU_ERR_ARGS;
+  if (pk_len != 48 && pk_len != 96) return BLSGPU_ERR_ARGS;
+  if (n == 0) return BLSGPU_OK;
+  if (!enter(ctx)) return BLSGPU_ERR_CLOSED;
+  Device* d = ctx->devs[0];
+  int rc = BLSGPU_OK;
+  try {
+    std::lock_guard<std::mutex> hl(d->helper_mu);
+    HIPCHK(hipSetDevice(d->id));
+    const size_t o_out = al256((size_t)n * stride), o_st = al256(o_out + (size_t)n * 96), total = o_st + n;
+    Slot& sl = d->helper;
+    sl.d_in.ensure(total);
+    hipStream_t s = d->table_stream;
+    uint8_t* din = sl.d_in.p;
+    HIPCHK(hipMemcpyAsync(din, pks, (size_t)n * stride, hipMemcpyHostToDevice, s));
+    launch_key_validate(din, n, pk_len, stride, din + o_out, reinterpret_cast<int8_t*>(din + o_st), s);
+    HIPCHK(hipGetLastError());
+    if (out96) HIPCHK(hipMemcpyAsync(out96, din + o_out, (size_t)n * 96, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(status, din + o_st, n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  } catch (HipError&) {
+    rc = BLSGPU_DEVICE_ERROR;
+  }
+  leave(ctx);
+  return rc;
+}
+
+int blsgpu_signing_roots(blsgpu_ctx* ctx, int kind, uint32_t n, const uint8_t* objects, uint32_t object_stride,
+                         const uint8_t* domains, uint32_t domain_stride, uint8_t* out32) {
+  if (!ctx || ctx->devs.empty() || !objects || !domains || !out32) return BLSGPU_ERR_ARGS;
+  const uint32_t obj_len = kind == BLSGPU_ROOT_OBJECT ? 32 : (kind == BLSGPU_ROOT_ATTESTATION_DATA ? 128 : 0);
+  if (!obj_len || object_stride < obj_len || (domain_stride != 0 && domain_stride < 32)) return BLSGPU_ERR_ARGS;
+  if (n == 0) return BLSGPU_OK;
+  if (!enter(ctx)) return BLSGPU_ERR_CLOSED;
+  Device* d = ctx->devs[0];
+  int rc = BLSGPU_OK;
+  try {
+    std::lock_guard<std::mutex> hl(d->helper_mu);
+    HIPCHK(hipSetDevice(d->id));
+    const size_t dom_bytes = (size_t)(domain_stride ? n : 1) * (domain_stride ? domain_stride : 32);
+    const size_t o_dom = al256((size_t)n * object_stride), o_out = al256(o_dom + dom_bytes), total = o_out + 32 * (size_t)n;
+    Slot& sl = d->helper;
+    sl.d_in.ensure(total);
+    hipStream_t s = d->table_stream;
+    uint8_t* din = sl.d_in.p;
+    HIPCHK(hipMemcpyAsync(din, objects, (size_t)n * object_stride, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(din + o_dom, domains, dom_bytes, hipMemcpyHostToDevice, s));
+    launch_signing_roots(kind, din, n, object_stride, din + o_dom, domain_stride, din + o_out, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out32, din + o_out, 32 * (size_t)n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  } catch (HipError&) {
+    rc = BLSGPU_DEVICE_ERROR;
+  }
+  leave(ctx);
+  return rc;
+}
+
 int blsgpu_debug_op(blsgpu_ctx* ctx, int op, uint32_t n, const uint8_t* in, uint32_t in_stride, uint8_t* out,
                     uint32_t out_stride, int32_t* status) {
   if (!ctx || ctx->devs.empty() || !in || !out || !status) return BLSGPU_ERR_ARGS;
   if (n == 0) return BLSGPU_OK;
+  if (!enter(ctx)) return BLSGPU_ERR_CLOSED;
   Device* d = ctx->devs[0];
-  Slot* sl = d->acquire();
   uint8_t *din = nullptr, *dout = nullptr;
   int32_t* dst = nullptr;
   int rc = BLSGPU_OK;
   try {
+    std::lock_guard<std::mutex> hl(d->helper_mu);
     HIPCHK(hipSetDevice(d->id));
+    hipStream_t s = d->table_stream;
     HIPCHK(hipMalloc((void**)&din, (size_t)n * in_stride));
     HIPCHK(hipMalloc((void**)&dout, (size_t)n * out_stride));
     HIPCHK(hipMalloc((void**)&dst, (size_t)n * 4));
-    HIPCHK(hipMemcpy(din, in, (size_t)n * in_stride, hipMemcpyHostToDevice));
-    HIPCHK(hipMemset(dout, 0, (size_t)n * out_stride));
-    launch_debug_op(op, n, din, in_stride, dout, out_stride, dst, sl->stream);
+    HIPCHK(hipMemcpyAsync(din, in, (size_t)n * in_stride, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(dout, 0, (size_t)n * out_stride, s));
+    launch_debug_op(op, n, din, in_stride, dout, out_stride, dst, s);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(sl->stream));
-    HIPCHK(hipMemcpy(out, dout, (size_t)n * out_stride, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(status, dst, (size_t)n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(out, dout, (size_t)n * out_stride, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(status, dst, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
   } catch (HipError&) {
     rc = BLSGPU_DEVICE_ERROR;
   }
   if (din) (void)hipFree(din);
   if (dout) (void)hipFree(dout);
   if (dst) (void)hipFree(dst);
-  d->release(sl);
+  leave(ctx);
   return rc;
 }
 

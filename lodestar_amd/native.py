@@ -33,7 +33,13 @@ EXPORTED_SYMBOLS = [
     "blsgpu_set_option",
     "blsgpu_code_name",
     "blsgpu_debug_op",
+    "blsgpu_aggregate_pubkeys",
+    "blsgpu_key_validate",
+    "blsgpu_signing_roots",
+    "blsgpu_shard_jobs",
 ]
+ROOT_OBJECT = 0
+ROOT_ATTESTATION_DATA = 1
 
 
 class Batch(ctypes.Structure):
@@ -61,6 +67,8 @@ class Stats(ctypes.Structure):
         ("devices_used", ctypes.c_uint32),
         ("device_ms", ctypes.c_double),
         ("stage_ms", ctypes.c_double * 8),
+        ("unique_messages", ctypes.c_uint32),
+        ("pairing_units", ctypes.c_uint32),
     ]
 
 
@@ -107,6 +115,11 @@ def load():
     lib.blsgpu_debug_op.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                     ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     lib.blsgpu_debug_op.restype = ctypes.c_int
+    vp, u32 = ctypes.c_void_p, ctypes.c_uint32
+    lib.blsgpu_aggregate_pubkeys.argtypes = [vp, ctypes.POINTER(Batch), vp, u32, vp]
+    lib.blsgpu_key_validate.argtypes = [vp, u32, vp, u32, u32, vp, vp]
+    lib.blsgpu_signing_roots.argtypes = [vp, ctypes.c_int, u32, vp, u32, vp, u32, vp]
+    lib.blsgpu_shard_jobs.argtypes = [vp, vp, u32, u32, vp]
     _lib = lib
     return lib
 
@@ -114,6 +127,63 @@ def load():
 def code_name(code: int) -> str:
     n = load().blsgpu_code_name(code)
     return n.decode() if n else f"BLSGPU_{code}"
+
+
+def shard_jobs(job_first_set, n_parts, set_pk_first=None):
+    """The runtime's sharding rule (C-ABI blsgpu_shard_jobs, pure host code): [(job_begin, job_end)]."""
+    jfs = np.ascontiguousarray(job_first_set, dtype=np.uint32)
+    spf = None if set_pk_first is None else np.ascontiguousarray(set_pk_first, dtype=np.uint32)
+    out = np.zeros(n_parts + 1, np.uint32)
+    rc = load().blsgpu_shard_jobs(jfs.ctypes.data, None if spf is None else spf.ctypes.data, len(jfs) - 1, n_parts,
+                                  out.ctypes.data)
+    if rc != OK:
+        raise ValueError(f"blsgpu_shard_jobs -> {code_name(rc)}")
+    return [(int(out[k]), int(out[k + 1])) for k in range(n_parts)]
+
+
+def _u8(b):
+    return np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else np.ascontiguousarray(b)
+
+
+def make_batch(job_first_set, sigs, sig_len, msgs, pk_bytes=None, set_pk_first=None, pk_index=None,
+               job_flags=None, sig_stride=None, seed=0x4C4F444553544152):
+    """blsgpu_batch over numpy/bytes arrays: (Batch, keep-alive list).  Modes: pk_bytes alone (one key per
+    set), pk_bytes + set_pk_first (bytes aggregate), set_pk_first + pk_index (device table)."""
+    job_first_set = np.ascontiguousarray(job_first_set, dtype=np.uint32)
+    sig_len = np.ascontiguousarray(sig_len, dtype=np.uint32)
+    n_sets = len(sig_len)
+    sigs, msgs = _u8(sigs), _u8(msgs)
+    if sig_stride is None:
+        sig_stride = (len(sigs) // n_sets) if n_sets else 96
+    keep = [job_first_set, sig_len, sigs, msgs]
+    b = Batch()
+    b.n_sets = n_sets
+    b.n_jobs = len(job_first_set) - 1
+    b.job_first_set = job_first_set.ctypes.data
+    if job_flags is not None:
+        job_flags = np.ascontiguousarray(job_flags, dtype=np.uint8)
+        keep.append(job_flags)
+        b.job_flags = job_flags.ctypes.data
+    if pk_bytes is not None:
+        pk = _u8(pk_bytes)
+        if len(pk) == 0:
+            pk = np.zeros(1, np.uint8)
+        keep.append(pk)
+        b.pk_bytes = pk.ctypes.data
+    if set_pk_first is not None:
+        set_pk_first = np.ascontiguousarray(set_pk_first, dtype=np.uint32)
+        keep.append(set_pk_first)
+        b.set_pk_first = set_pk_first.ctypes.data
+    if pk_index is not None:
+        pk_index = np.ascontiguousarray(pk_index, dtype=np.uint32)
+        keep.append(pk_index)
+        b.pk_index = pk_index.ctypes.data if len(pk_index) else set_pk_first.ctypes.data
+    b.msgs = msgs.ctypes.data if len(msgs) else 0
+    b.sigs = sigs.ctypes.data if len(sigs) else 0
+    b.sig_len = sig_len.ctypes.data if len(sig_len) else 0
+    b.sig_stride = sig_stride
+    b.seed = seed
+    return b, keep
 
 
 class Context:
@@ -165,44 +235,49 @@ class Context:
     def verify_raw(self, job_first_set, sigs, sig_len, msgs, pk_bytes=None, set_pk_first=None, pk_index=None,
                    job_flags=None, sig_stride=None, seed=0x4C4F444553544152):
         """Low-level call: numpy/bytes arrays in, (job_result int8 array, Stats) out."""
-        job_first_set = np.ascontiguousarray(job_first_set, dtype=np.uint32)
-        n_jobs = len(job_first_set) - 1
-        sig_len = np.ascontiguousarray(sig_len, dtype=np.uint32)
-        n_sets = len(sig_len)
-        if sig_stride is None:
-            sig_stride = (len(sigs) // n_sets) if n_sets else 96
-        sigs = np.frombuffer(bytes(sigs), dtype=np.uint8) if not isinstance(sigs, np.ndarray) else sigs
-        msgs = np.frombuffer(bytes(msgs), dtype=np.uint8) if not isinstance(msgs, np.ndarray) else msgs
-        keep = [job_first_set, sig_len, sigs, msgs]
-        b = Batch()
-        b.n_sets = n_sets
-        b.n_jobs = n_jobs
-        b.job_first_set = job_first_set.ctypes.data
-        if job_flags is not None:
-            job_flags = np.ascontiguousarray(job_flags, dtype=np.uint8)
-            keep.append(job_flags)
-            b.job_flags = job_flags.ctypes.data
-        if pk_bytes is not None:
-            pk = np.frombuffer(bytes(pk_bytes), dtype=np.uint8) if not isinstance(pk_bytes, np.ndarray) else pk_bytes
-            keep.append(pk)
-            b.pk_bytes = pk.ctypes.data
-        else:
-            set_pk_first = np.ascontiguousarray(set_pk_first, dtype=np.uint32)
-            pk_index = np.ascontiguousarray(pk_index, dtype=np.uint32)
-            keep += [set_pk_first, pk_index]
-            b.set_pk_first = set_pk_first.ctypes.data
-            b.pk_index = pk_index.ctypes.data if len(pk_index) else set_pk_first.ctypes.data
-        b.msgs = msgs.ctypes.data
-        b.sigs = sigs.ctypes.data
-        b.sig_len = sig_len.ctypes.data
-        b.sig_stride = sig_stride
-        b.seed = seed
-        res = np.zeros(max(n_jobs, 1), dtype=np.int8)
+        b, keep = make_batch(job_first_set, sigs, sig_len, msgs, pk_bytes, set_pk_first, pk_index, job_flags,
+                             sig_stride, seed)
+        res = np.zeros(max(b.n_jobs, 1), dtype=np.int8)
         st = Stats()
         rc = self._lib.blsgpu_verify(self.h, ctypes.byref(b), res.ctypes.data, ctypes.byref(st))
         if rc != OK:
             raise RuntimeError(f"blsgpu_verify -> {code_name(rc)}")
-        return res[:n_jobs], st
+        return res[: b.n_jobs], st
+
+    def aggregate_pubkeys(self, pk_bytes=None, set_pk_first=None, pk_index=None, out_len=96):
+        """PublicKey.aggregate(...).toBytes() per set on the GPU: (list of bytes, status int8 array)."""
+        n = (len(set_pk_first) - 1) if set_pk_first is not None else len(pk_bytes) // 96
+        b, keep = make_batch(np.array([0, n]), b"", np.zeros(n, np.uint32), b"", pk_bytes, set_pk_first, pk_index)
+        out = np.zeros(max(n, 1) * out_len, np.uint8)
+        st = np.zeros(max(n, 1), np.int8)
+        rc = self._lib.blsgpu_aggregate_pubkeys(self.h, ctypes.byref(b), out.ctypes.data, out_len, st.ctypes.data)
+        if rc != OK:
+            raise RuntimeError(f"blsgpu_aggregate_pubkeys -> {code_name(rc)}")
+        return [out[out_len * i: out_len * (i + 1)].tobytes() for i in range(n)], st[:n]
+
+    def key_validate(self, pks: bytes, pk_len: int):
+        """KeyValidate on the GPU: (96-byte uncompressed keys, status int8 array)."""
+        n = len(pks) // pk_len
+        src = _u8(pks)
+        out = np.zeros(max(n, 1) * 96, np.uint8)
+        st = np.zeros(max(n, 1), np.int8)
+        rc = self._lib.blsgpu_key_validate(self.h, n, src.ctypes.data, pk_len, pk_len, out.ctypes.data, st.ctypes.data)
+        if rc != OK:
+            raise RuntimeError(f"blsgpu_key_validate -> {code_name(rc)}")
+        return out[: 96 * n].tobytes(), st[:n]
+
+    def signing_roots(self, kind: int, objects: bytes, domains: bytes):
+        """computeSigningRoot on the GPU: one domain for all (32 B) or one per object."""
+        obj_len = 32 if kind == ROOT_OBJECT else 128
+        n = len(objects) // obj_len
+        o, d = _u8(objects), _u8(domains)
+        dstride = 0 if len(domains) == 32 else 32
+        out = np.zeros(max(n, 1) * 32, np.uint8)
+        rc = self._lib.blsgpu_signing_roots(self.h, kind, n, o.ctypes.data, obj_len, d.ctypes.data, dstride,
+                                            out.ctypes.data)
+        if rc != OK:
+            raise RuntimeError(f"blsgpu_signing_roots -> {code_name(rc)}")
+        return [out[32 * i: 32 * i + 32].tobytes() for i in range(n)]
 
     def debug_op(self, op: int, inputs: bytes, in_stride: int, out_stride: int):
         n = len(inputs) // in_stride

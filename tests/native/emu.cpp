@@ -94,6 +94,14 @@ void emu_stage_pk_aggregate(const uint8_t* pk96, int n) {
   for (int i = 0; i < n; i++) acc = jac_add_aff(acc, (i & 1) ? p : p2);
 }
 #endif
+// KeyValidate (48- or 96-byte pubkey) -> status, 96-byte uncompressed
+int emu_key_validate(const uint8_t* b, uint32_t len, uint8_t* out96) {
+  g1a p;
+  int st = pk_key_validate(b, len, p);
+  if (st == 0) g1a_to_be96(p, out96);
+  return st;
+}
+int emu_g1_in_subgroup(const uint8_t* pk96) { return g1_in_subgroup(load_g1(pk96)) ? 1 : 0; }
 void emu_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp_to_be48(fp_mul(load_mont(a), load_mont(b)), out); }
 void emu_fp_sqr(const uint8_t* a, uint8_t* out) { fp_to_be48(fp_sqr(load_mont(a)), out); }
 void emu_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* out) { fp_to_be48(fp_add(load_mont(a), load_mont(b)), out); }

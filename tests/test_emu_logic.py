@@ -173,3 +173,29 @@ def test_sig_decode_classes():
         assert got == bls.classify_signature(b) == want, (b.hex(), got, want)
     codes = set(cases.values())
     assert bls.BLST_POINT_NOT_ON_CURVE in codes and bls.BLST_POINT_NOT_IN_GROUP in codes
+
+
+def test_key_validate_matches_c_oracle():
+    """Device KeyValidate (decompress + phi(P) == -[z^2]P subgroup check) vs the C oracle's definitional
+    [r]P == O check, on the reference's cachedKeys (cli/test/utils/cachedKeys.ts:15-26) and on adversarial
+    48-byte candidates covering every error class."""
+    from oracle import cpu
+
+    L = lib()
+    out = ctypes.create_string_buffer(96)
+    cands = [bytes.fromhex(h) for h in (
+        "8be678633e927aa0435addad5dcd5283fef6110d91362519cd6d43e61f6c017d724fa579cc4b2972134e050b6ba120c0",
+        "8e602f8ec17777c22f465f9b4707c2840647790f15f5c33bd8850f274d5c320850105639960ae4effe57aa5dd279bb98")]
+    cands += [bytes([0xC0]) + bytes(47), bytes(48), bytes([0x9F]) + bytes([0xFF]) * 47]
+    cands += [bytes([0x80 | (t & 0x20)]) + bytes(45) + t.to_bytes(2, "big") for t in range(1, 120)]
+    seen = set()
+    for c in cands:
+        st = L.emu_key_validate(c, len(c), out)
+        want = cpu.key_validate(c)
+        assert st == want, c.hex()
+        seen.add(st)
+        if st == 0:
+            assert cpu.pk_decode(c) == (0, out.raw)
+            assert L.emu_key_validate(out.raw, 96, out) == 0
+    assert {0, bls.BLST_BAD_ENCODING, bls.BLST_POINT_NOT_ON_CURVE, bls.BLST_POINT_NOT_IN_GROUP,
+            bls.BLST_PK_IS_INFINITY} <= seen

@@ -20,7 +20,7 @@ def ctx():
 
 
 def run(ctx, w, seed=bench.SEED, **over):
-    call = {k: v for k, v in w.items() if k != "expected"}
+    call = {k: v for k, v in w.items() if k not in ("expected", "pks_table")}
     call.update(over)
     res, st = ctx.verify_raw(**call, seed=seed)
     return res, st

@@ -34,6 +34,19 @@ def test_shard_jobs_single_process_properties():
     assert shard_jobs([0], 4) == [(0, 0)] * 4  # no jobs
 
 
+def test_cpp_and_python_shard_rules_agree():
+    """The C-ABI blsgpu_shard_jobs (the rule the runtime applies over the devices of one process) and
+    lodestar_amd/shard.py (the rule ranks apply under torch.distributed) give identical ranges."""
+    from lodestar_amd.native import shard_jobs as cpp_shard
+
+    for seed in range(6):
+        jfs, spf = workload(seed, n_jobs=300 + 97 * seed)
+        for n in (1, 2, 3, 4, 7, 8):
+            assert cpp_shard(jfs, n, spf) == shard_jobs(jfs, n, spf)
+            assert cpp_shard(jfs, n) == shard_jobs(jfs, n)
+    assert cpp_shard([0], 3) == shard_jobs([0], 3) == [(0, 0)] * 3
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -41,6 +54,9 @@ def _worker(rank, world, port, q):
     try:
         jfs, spf = workload()
         mine = shard_jobs(jfs, world, spf)[rank]
+        from lodestar_amd.native import shard_jobs as cpp_shard
+
+        assert cpp_shard(jfs, world, spf)[rank] == mine
         # every rank gathers every rank's independently computed range
         got = [None] * world
         dist.all_gather_object(got, mine)

@@ -1,0 +1,8 @@
+# usage: bash tools/gpurun/r02_tests.sh TAG  -- GPU parity tests (verbose, per-test timeout), then smoke
+set -e
+TAG=$1; shift
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export GPU_MAX_HW_QUEUES=8
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1
