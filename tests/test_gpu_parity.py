@@ -89,7 +89,7 @@ def corrupted_single_sets(n, tag, rng):
     bad = rng.choice(n, size=max(8, n // 100), replace=False)
     adv = adversarial_sigs()
     kinds = ["wrong_msg", "swap", "infinity", "size"] + sorted(adv)
-    for k, i in enumerate(bad):
+    for k, i in enumerate(bad.tolist()):
         kind = kinds[k % len(kinds)]
         if kind == "wrong_msg":
             msgs[i] = msg(i, tag + b"other")
@@ -122,7 +122,7 @@ def test_full_size_single_sets_vs_oracle(ctx, n, tag):
     base = dict(sigs=sigs, sig_len=sig_len, msgs=b"".join(msgs), sig_stride=192)
     # gossip shape: one batchable job per set, bytes mode
     got, st = compare(ctx, job_first_set=np.arange(n + 1), pk_bytes=pks, job_flags=np.ones(n), **base)
-    assert (got == 1).sum() > n * 0.95 and (got == 0).sum() >= 2 and (got < 0).sum() >= 4
+    assert (got == 1).sum() >= n - max(8, n // 100) and (got == 0).sum() >= 2 and (got < 0).sum() >= 4
     assert st.batch_retries >= 1
     # table mode (the bench's C2 shape)
     ctx.upload_pubkeys(0, pks)
