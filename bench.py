@@ -307,6 +307,7 @@ def main():
     ap.add_argument("--group-sets", type=int, default=256)
     ap.add_argument("--inflight", type=int, default=12,
                     help="verifySignatureSets calls in flight per GPU (runtime slots); 1 = strictly serial")
+    ap.add_argument("--miller-k", type=int, default=2, help="pairings per Miller accumulator (shared squarings)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
@@ -337,6 +338,7 @@ def main():
     ctx = Context(devices)
     ctx.set_option("group_sets", args.group_sets)
     ctx.set_option("slots", max(1, args.inflight))
+    ctx.set_option("miller_k", args.miller_k)
     work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev)
     call = dict(work)
     expected = call.pop("expected", None)
@@ -390,6 +392,7 @@ def main():
         lat.append((time.perf_counter() - t1) * 1e3)
     out = {
         "metric": "verified signature sets/sec (node)",
+        "miller_k": args.miller_k,
         "value": round(value, 2),
         "unit": "sets/s",
         "n_gpus": n_gpus,

@@ -101,6 +101,7 @@ typedef struct blsgpu_stats {
   double stage_ms[8];
   uint32_t unique_messages; /* distinct signing roots hashed to G2 */
   uint32_t pairing_units;   /* Miller loops of the batch pass (sets, or same-message units) */
+  uint32_t miller_chunks;   /* Miller accumulators of the batch pass (miller_k pairings share squarings) */
 } blsgpu_stats;
 
 /* Create a context on the given HIP devices (NULL / n <= 0: every visible device).  Each device gets 4
@@ -135,7 +136,8 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
 
 /* Tunables: "group_sets" (sets per batch group before a new one opens, default 256), "slots" (runtime slots
  * per device, only grows, default 4), "max_devices" (devices one call may shard over, default all),
- * "dedupe" (message dedupe + same-message pairing, 0/1, default 1), "profile" (per-stage kernel times in
+ * "dedupe" (message dedupe + same-message pairing, 0/1, default 1), "miller_k" (pairings per Miller
+ * accumulator sharing its Fp12 squarings, 1..64, default 2), "profile" (per-stage kernel times in
  * blsgpu_stats.stage_ms, 0/1).  Applies to calls submitted afterwards. */
 int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value);
 

@@ -33,7 +33,11 @@
 //     loop, the final exponentiation, decoders) are real device functions (BLS_BIG / BLS_HDNI), where the
 //     argument round trip is negligible next to their work.
 #define BLS_INL __device__ __forceinline__
+#if BLS_INLINE_BIG
+#define BLS_BIG __device__ __forceinline__
+#else
 #define BLS_BIG __device__ __noinline__
+#endif
 #define BLS_HDNI BLS_BIG
 #define BLS_FN BLS_INL
 #else

@@ -2,7 +2,7 @@
 //
 // A batch group is a contiguous range of clean jobs checked with ONE final exponentiation:
 //   prod_i e(r_i pk_i, H(m_i)) * e(-g1, sum_i r_i sig_i) == 1
-// The Miller values (per set, or per same-message unit) were computed by k_miller_acc; here
+// The Miller values (chunks of sets or same-message units) were computed by k_miller_acc; here
 //   k_group_reduce   one wave per group: S = sum r_i sig_i (G2) and F = prod f (Fp12), each lane a strided
 //                    partial, then a 6-level LDS tree (64 -> 1)
 //   k_group_check    one 128-lane workgroup per group: FinalExp(F * MillerLoop(-g1, S)) == 1, as
@@ -28,8 +28,7 @@ __global__ __launch_bounds__(WAVE) void k_job_mask(PipelineBuffers b) {
 }
 
 __global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const uint32_t* set_ranges,
-                                                       const uint32_t* f_ranges, const uint32_t* f_src,
-                                                       bool f_per_set, uint32_t ng, uint32_t* S_out,
+                                                       const uint32_t* f_ranges, uint32_t ng, uint32_t* S_out,
                                                        uint32_t* F_out) {
   __shared__ uint32_t red[WAVE * W_FP12];
   const uint32_t g = blockIdx.x, lane = threadIdx.x;
@@ -49,15 +48,14 @@ __global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const 
     }
     if (lane == 0) st_g2j(S_out, ng, g, S);
   }
-  // ---- F = prod of the group's Miller values (per-set values: included sets only)
+  // ---- F = prod of the group's Miller chunks
   const uint32_t first = f_ranges[2 * g], last = f_ranges[2 * g + 1];
   fp12 F = fp12_one();
   bool any = false;
-  for (uint32_t i = first + lane; i < last; i += WAVE)
-    if (!f_per_set || b.include[i]) {
-      F = any ? fp12_mul(F, ld_fp12(f_src, b.n, i)) : ld_fp12(f_src, b.n, i);
-      any = true;
-    }
+  for (uint32_t i = first + lane; i < last; i += WAVE) {
+    F = any ? fp12_mul(F, ld_fp12(b.f_chunk, b.n, i)) : ld_fp12(b.f_chunk, b.n, i);
+    any = true;
+  }
 #pragma unroll 1
   for (int s = WAVE / 2; s >= 1; s >>= 1) {
     if (lane >= (uint32_t)s && lane < (uint32_t)(2 * s)) st_fp12(red, WAVE, lane - s, F);
@@ -106,10 +104,8 @@ void launch_job_mask(const PipelineBuffers& b, hipStream_t s) {
   if (b.n_jobs) hipLaunchKernelGGL(k_job_mask, grid_for(b.n_jobs), dim3(WAVE), 0, s, b);
 }
 void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
-                         bool f_per_set, uint32_t ng, uint32_t* S, uint32_t* F, hipStream_t s) {
-  if (ng)
-    hipLaunchKernelGGL(k_group_reduce, dim3(ng), dim3(WAVE), 0, s, b, set_ranges, f_ranges,
-                       (const uint32_t*)(f_per_set ? b.f_set : b.f_unit), f_per_set, ng, S, F);
+                         uint32_t ng, uint32_t* S, uint32_t* F, hipStream_t s) {
+  if (ng) hipLaunchKernelGGL(k_group_reduce, dim3(ng), dim3(WAVE), 0, s, b, set_ranges, f_ranges, ng, S, F);
 }
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s) {
   if (ng) hipLaunchKernelGGL(k_group_check, dim3(ng), dim3(GTW_LANES), 0, s, S, F, ng, ok);

@@ -3,10 +3,11 @@
 //                   line (l0, c1, c4) goes to HBM, SoA limb-major (step s, word w of message u at
 //                   lines[(s * W_LINE + w) * nm + u]: coalesced).  Lines depend on H(m) only, so every set
 //                   and unit signing the same root shares them;
-//   k_miller_acc:   one lane per pairing unit: f = prod_s line_s(P) with the squarings, from the stored lines;
-//                   writes conj(f).  A unit is either one set (P = r_i pk_i) or, with same-message merging,
-//                   the included sets of one batch group that sign the same root (P = sum r_i pk_i): the
-//                   pairing is bilinear, so prod_i e(r_i pk_i, H(m)) = e(sum_i r_i pk_i, H(m)).
+//   k_miller_acc:   one lane per chunk of <= K pairings of one batch group: f = prod_s prod_items line_s(P)
+//                   with shared squarings, from the stored lines; writes conj(f).  An item is either one set
+//                   (P = r_i pk_i) or, with same-message merging, a unit: the included sets of one batch
+//                   group that sign the same root (P = sum r_i pk_i; the pairing is bilinear, so
+//                   prod_i e(r_i pk_i, H(m)) = e(sum_i r_i pk_i, H(m))).
 // Line traffic is 68 x 84 words = 22.8 KB per message (HBM-cheap next to ~5,200 Montgomery products).
 #include "k_common.hpp"
 
@@ -38,50 +39,50 @@ STAGE_KERNEL void k_miller_lines(PipelineBuffers b) {
   }
 }
 
-// UNITS: lane u is pairing unit u (P = unit_p[u], f -> f_unit[u]).  Otherwise lane u is set
-// i = set_list ? set_list[u] : u (P = pk_aff[i], f -> f_set[i]); a set outside the batch equation gets f = 1.
+// One lane per chunk: f = prod over the chunk's items of f_{|z|,Q_item}(P_item), with ONE Fp12 squaring per
+// doubling step for the whole chunk (the multi-pairing form of blst's miller_loop_n): K items cost
+// 63 squarings + 68 K line multiplications instead of K (63 + 68).  UNITS: item u is pairing unit u
+// (P = unit_p[u]); otherwise item i is a set (P = r_i pk_i, only if it enters the batch equation).
 template <bool UNITS>
-STAGE_KERNEL void k_miller_acc(PipelineBuffers b, uint32_t n, const uint32_t* set_list) {
-  uint32_t u = blockIdx.x * WAVE + threadIdx.x;
-  if (u >= n) return;
-  uint32_t i, m;
-  bool active;
-  const uint32_t* psrc;
-  if (UNITS) {
-    i = u;
-    m = b.unit_msg[u];
-    active = b.unit_ok[u] != 0;
-    psrc = b.unit_p;
-  } else {
-    i = set_list ? set_list[u] : u;
-    m = b.msg_idx[i];
-    active = b.include[i] != 0;
-    psrc = b.pk_aff;
-  }
-  active = active && !(b.mflags[m] & MF_H_INF);
+STAGE_KERNEL void k_miller_acc(PipelineBuffers b) {
+  const uint32_t c = blockIdx.x * WAVE + threadIdx.x;
+  if (c >= b.n_chunks) return;
+  const uint32_t k0 = b.chunk_first[c], k1 = b.chunk_first[c + 1];
   fp12 f = fp12_one();
-  if (active) {
-    const g1a P = ld_g1a(psrc, b.n, i);
-    int bit = 62;
-    bool add_next = false;
+  int bit = 62;
+  bool add_next = false;
 #pragma unroll 1
-    for (int s = 0; s < MILLER_STEPS; s++) {
-      const uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
+  for (int s = 0; s < MILLER_STEPS; s++) {
+    if (!add_next && s != 0) f = fp12_sqr(f);
+    const uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
+#pragma unroll 1
+    for (uint32_t k = k0; k < k1; k++) {
+      const uint32_t i = b.chunk_items[k];
+      uint32_t m;
+      bool active;
+      if (UNITS) {
+        m = b.unit_msg[i];
+        active = b.unit_ok[i] != 0;
+      } else {
+        m = b.msg_idx[i];
+        active = b.include[i] != 0;
+      }
+      if (!active || (b.mflags[m] & MF_H_INF)) continue;
+      const g1a P = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
       line3 L;
       L.l0 = ld_fp2(o, b.nm, m, 0);
       L.c1 = ld_fp2(o, b.nm, m, 2 * W_FP);
       L.c4 = ld_fp2(o, b.nm, m, 4 * W_FP);
-      f = miller_acc_step(f, s, add_next, L, P.x, P.y);
-      if (!add_next) {
-        add_next = (BLS_Z_ABS >> bit) & 1ull;
-        bit--;
-      } else {
-        add_next = false;
-      }
+      f = fp12_mul_by_014(f, L.l0, fp2_mul_fp(L.c1, P.x), fp2_mul_fp(L.c4, P.y));
     }
-    f = fp12_conj(f);
+    if (!add_next) {
+      add_next = (BLS_Z_ABS >> bit) & 1ull;
+      bit--;
+    } else {
+      add_next = false;
+    }
   }
-  st_fp12(UNITS ? b.f_unit : b.f_set, b.n, i, f);
+  st_fp12(b.f_chunk, b.n, c, fp12_conj(f));
 }
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
@@ -89,10 +90,10 @@ static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 void launch_miller_lines(const PipelineBuffers& b, hipStream_t s) {
   if (b.n_umsg) hipLaunchKernelGGL(k_miller_lines, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
 }
-void launch_miller_acc(const PipelineBuffers& b, bool units, uint32_t n, const uint32_t* set_list, hipStream_t s) {
-  if (!n) return;
+void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s) {
+  if (!b.n_chunks) return;
   if (units)
-    hipLaunchKernelGGL(k_miller_acc<true>, grid_for(n), dim3(WAVE), 0, s, b, n, set_list);
+    hipLaunchKernelGGL(k_miller_acc<true>, grid_for(b.n_chunks), dim3(WAVE), 0, s, b);
   else
-    hipLaunchKernelGGL(k_miller_acc<false>, grid_for(n), dim3(WAVE), 0, s, b, n, set_list);
+    hipLaunchKernelGGL(k_miller_acc<false>, grid_for(b.n_chunks), dim3(WAVE), 0, s, b);
 }

@@ -55,8 +55,12 @@ struct PipelineBuffers {
   uint32_t* pk_aff;   // W_G1A, per set (r * pk, affine)
   uint32_t* rsig;     // W_G2J, per set
   uint32_t* unit_p;   // W_G1A, per unit (stride n)
-  uint32_t* f_set;    // W_FP12, per set: Miller values (per-set mode and the fallback)
-  uint32_t* f_unit;   // W_FP12, per unit (stride n)
+  // Miller chunks: chunk c multiplies the Miller values of items chunk_items[chunk_first[c] ..
+  // chunk_first[c+1]) (sets, or units) into ONE accumulator with shared squarings -> f_chunk[c]
+  uint32_t n_chunks;
+  const uint32_t* chunk_first;
+  const uint32_t* chunk_items;
+  uint32_t* f_chunk;  // W_FP12, per chunk (stride n)
   uint32_t* lines;    // Miller lines, per message: MILLER_STEPS x W_LINE words, step-major SoA (stride nm)
   uint8_t* flags;     // [n]: sig flags
   uint8_t* mflags;    // [nm]: message flags
@@ -77,14 +81,14 @@ void launch_job_mask(const PipelineBuffers& b, hipStream_t s);
 void launch_unit_aggregate(const PipelineBuffers& b, hipStream_t s);
 // Miller lines of every unique message
 void launch_miller_lines(const PipelineBuffers& b, hipStream_t s);
-// Miller values: units (f_unit) when `units`, else per set (f_set) for n sets -- all sets when set_list is
-// null, else the listed ones
-void launch_miller_acc(const PipelineBuffers& b, bool units, uint32_t n, const uint32_t* set_list, hipStream_t s);
+// Miller values of the chunks (items are units when `units`, else sets): f_chunk[c] = prod over the chunk's
+// active items of MillerLoop(P_item, H(m_item)), one lane per chunk, the Fp12 squarings shared
+void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s);
 // Batch groups: group g covers sets [set_ranges[2g], set_ranges[2g+1]) (S over included sets) and Miller
-// values [f_ranges[2g], f_ranges[2g+1]) of f (per-set values count only for included sets when f_per_set).
-// reduce: S_g = sum r_i sig_i (W_G2J SoA, stride n_groups), F_g = prod f (W_FP12 SoA, stride n_groups)
+// chunks [f_ranges[2g], f_ranges[2g+1]).
+// reduce: S_g = sum r_i sig_i (W_G2J SoA, stride n_groups), F_g = prod f_chunk (W_FP12 SoA, stride n_groups)
 void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
-                         bool f_per_set, uint32_t n_groups, uint32_t* S, uint32_t* F, hipStream_t s);
+                         uint32_t n_groups, uint32_t* S, uint32_t* F, hipStream_t s);
 // check: ok_g = FinalExp(F_g * MillerLoop(-g1, S_g)) == 1
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t n_groups, uint8_t* ok, hipStream_t s);
 // pubkey table upload: decode 96-byte affine encodings into table entries, per-entry status

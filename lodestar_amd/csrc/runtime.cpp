@@ -148,7 +148,19 @@ struct Options {  // snapshot taken at the start of each call
   int64_t max_devices = 64;
   bool profile = false;
   bool dedupe = true;
+  int64_t miller_k = 2;  // pairings per Miller accumulator (shared squarings)
 };
+
+// Splits item ranges into Miller chunks of <= k items: appends to first/items, returns [chunk_begin, end)
+inline std::pair<uint32_t, uint32_t> add_chunks(std::vector<uint32_t>& first, std::vector<uint32_t>& items,
+                                                uint32_t a, uint32_t e, uint32_t k, const uint32_t* map = nullptr) {
+  const uint32_t c0 = (uint32_t)first.size() - 1;
+  for (uint32_t x = a; x < e; x += k) {
+    for (uint32_t y = x; y < std::min(e, x + k); y++) items.push_back(map ? map[y] : y);
+    first.push_back((uint32_t)items.size());
+  }
+  return {c0, (uint32_t)first.size() - 1};
+}
 
 struct Shard {
   uint32_t job_begin, job_end;  // job range
@@ -361,6 +373,18 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     }
   }
   const uint32_t n_units = merged ? (uint32_t)unit_msg.size() : 0;
+  // Miller chunks of the batch pass: each group's items (sets, or units) in chunks of miller_k
+  const uint32_t mk = (uint32_t)std::max<int64_t>(1, opt.miller_k);
+  std::vector<uint32_t> chunk_first{0}, chunk_items, g_chunks(2 * (size_t)ng0);
+  chunk_items.reserve(n);
+  for (uint32_t g = 0; g < ng0; g++) {
+    const uint32_t a = merged ? g_unit_first[g] : job_sets(group_jobs[g].first).first;
+    const uint32_t e = merged ? g_unit_first[g + 1] : job_sets(group_jobs[g].second - 1).second;
+    const auto cr = add_chunks(chunk_first, chunk_items, a, e, mk);
+    g_chunks[2 * g] = cr.first;
+    g_chunks[2 * g + 1] = cr.second;
+  }
+  const uint32_t n_chunks = (uint32_t)chunk_first.size() - 1;
 
   // ---- stage inputs in the pinned arena and copy it to the device in one transfer ------------------------
   // arena (256-B aligned sections): scalars | job_first_set | sigs (192 B each) | sig_len | unique msgs |
@@ -371,7 +395,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
                o_franges = al256(o_ranges + (size_t)std::max(ng0, 1u) * 8),
                o_ufirst = al256(o_franges + (size_t)std::max(ng0, 1u) * 8),
                o_usets = al256(o_ufirst + (size_t)(n_units + 1) * 4), o_umsgi = al256(o_usets + (size_t)unit_sets.size() * 4),
-               o_pk = al256(o_umsgi + (size_t)n_units * 4);
+               o_cfirst = al256(o_umsgi + (size_t)n_units * 4), o_citems = al256(o_cfirst + (size_t)(n_chunks + 1) * 4),
+               o_pk = al256(o_citems + chunk_items.size() * 4);
   size_t in_bytes;
   if (table_mode)
     in_bytes = al256(o_pk + (size_t)(n + 1) * 4) + (size_t)npk * 4;
@@ -402,9 +427,11 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   for (uint32_t g = 0; g < ng0; g++) {
     hranges[2 * g] = job_sets(group_jobs[g].first).first;
     hranges[2 * g + 1] = job_sets(group_jobs[g].second - 1).second;
-    hfranges[2 * g] = merged ? g_unit_first[g] : hranges[2 * g];
-    hfranges[2 * g + 1] = merged ? g_unit_first[g + 1] : hranges[2 * g + 1];
+    hfranges[2 * g] = g_chunks[2 * g];
+    hfranges[2 * g + 1] = g_chunks[2 * g + 1];
   }
+  memcpy(hin + o_cfirst, chunk_first.data(), chunk_first.size() * 4);
+  memcpy(hin + o_citems, chunk_items.data(), chunk_items.size() * 4);
   if (merged) {
     memcpy(hin + o_ufirst, unit_first.data(), (size_t)(n_units + 1) * 4);
     memcpy(hin + o_usets, unit_sets.data(), unit_sets.size() * 4);
@@ -432,7 +459,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   sl.d_S.ensure((size_t)W_G2J * max_ranges);
   sl.d_F.ensure((size_t)W_FP12 * max_ranges);
   // work area: per set sig_aff, pk_jac, pk_aff, rsig, f_set (+ per unit unit_p, f_unit), per message h_aff
-  const size_t per_set = W_G2A + W_G1J + W_G1A + W_G2J + W_FP12 + (merged ? W_G1A + W_FP12 : 0);
+  const size_t per_set = W_G2A + W_G1J + W_G1A + W_G2J + W_FP12 + (merged ? W_G1A : 0);
   sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * W_G2A);
   sl.d_lines.ensure((size_t)nm * kMillerLineWords);
   hipStream_t s = sl.stream;
@@ -467,11 +494,13 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.pk_jac = w; w += (size_t)stride * W_G1J;
   pb.pk_aff = w; w += (size_t)stride * W_G1A;
   pb.rsig = w; w += (size_t)stride * W_G2J;
-  pb.f_set = w; w += (size_t)stride * W_FP12;
+  pb.f_chunk = w; w += (size_t)stride * W_FP12;
   if (merged) {
     pb.unit_p = w; w += (size_t)stride * W_G1A;
-    pb.f_unit = w; w += (size_t)stride * W_FP12;
   }
+  pb.n_chunks = n_chunks;
+  pb.chunk_first = reinterpret_cast<uint32_t*>(din + o_cfirst);
+  pb.chunk_items = reinterpret_cast<uint32_t*>(din + o_citems);
   pb.h_aff = w;
   pb.lines = sl.d_lines.p;
   uint8_t* const db = sl.d_bytes.p;
@@ -500,16 +529,12 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   launch_job_mask(pb, s);
   mark(5);
   launch_miller_lines(pb, s);
-  if (merged) {
-    launch_unit_aggregate(pb, s);
-    launch_miller_acc(pb, true, n_units, nullptr, s);
-  } else {
-    launch_miller_acc(pb, false, n, nullptr, s);
-  }
+  if (merged) launch_unit_aggregate(pb, s);
+  launch_miller_acc(pb, merged, s);
   mark(6);
   const uint32_t* d_ranges = reinterpret_cast<uint32_t*>(din + o_ranges);
   const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
-  launch_group_reduce(pb, d_ranges, d_franges, !merged, ng0, sl.d_S.p, sl.d_F.p, s);
+  launch_group_reduce(pb, d_ranges, d_franges, ng0, sl.d_S.p, sl.d_F.p, s);
   mark(7);
   launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, s);
   mark(8);
@@ -519,6 +544,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   st.groups += ng0;
   st.unique_messages += n_umsg;
   st.pairing_units += merged ? n_units : n;
+  st.miller_chunks += n_chunks;
   if (prof) {
     for (int k = 0; k < kStages; k++) {
       float ms = 0;
@@ -552,31 +578,38 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   }
 
   // ---- fallback: one parallel launch re-checks every clean job of every failed group -----------------------
+  // Each retried job gets its own set range (S) and its own Miller chunks (its sets, miller_k per chunk).
   if (!retry.empty()) {
     const uint32_t nr = (uint32_t)retry.size();
-    uint32_t n_list = 0;
-    if (merged) {  // per-set Miller values of the retried jobs' sets (units only exist per group)
-      for (uint32_t j : retry) n_list += job_sets(j).second - job_sets(j).first;
-    }
-    sl.h_list.ensure(2 * (size_t)nr + n_list);
-    sl.d_list.ensure(2 * (size_t)nr + n_list);
-    uint32_t* hl = sl.h_list.p;
+    std::vector<uint32_t> rfirst{0}, ritems, rr(2 * (size_t)nr), rf(2 * (size_t)nr);
     for (uint32_t q = 0; q < nr; q++) {
-      hl[2 * q] = job_sets(retry[q]).first;
-      hl[2 * q + 1] = job_sets(retry[q]).second;
+      const auto js = job_sets(retry[q]);
+      rr[2 * q] = js.first;
+      rr[2 * q + 1] = js.second;
+      const auto cr = add_chunks(rfirst, ritems, js.first, js.second, mk);
+      rf[2 * q] = cr.first;
+      rf[2 * q + 1] = cr.second;
     }
-    uint32_t* sets_list = hl + 2 * (size_t)nr;
-    uint32_t k = 0;
-    if (merged)
-      for (uint32_t j : retry)
-        for (uint32_t i = job_sets(j).first; i < job_sets(j).second; i++) sets_list[k++] = i;
+    const uint32_t nc = (uint32_t)rfirst.size() - 1;
+    const size_t words = 4 * (size_t)nr + rfirst.size() + ritems.size();
+    sl.h_list.ensure(words);
+    sl.d_list.ensure(words);
+    uint32_t* hl = sl.h_list.p;
+    memcpy(hl, rr.data(), rr.size() * 4);
+    memcpy(hl + 2 * (size_t)nr, rf.data(), rf.size() * 4);
+    memcpy(hl + 4 * (size_t)nr, rfirst.data(), rfirst.size() * 4);
+    memcpy(hl + 4 * (size_t)nr + rfirst.size(), ritems.data(), ritems.size() * 4);
     sl.d_ok.ensure(nr);
     sl.h_ok.ensure(nr);
     sl.d_S.ensure((size_t)W_G2J * nr);
     sl.d_F.ensure((size_t)W_FP12 * nr);
-    HIPCHK(hipMemcpyAsync(sl.d_list.p, hl, (2 * (size_t)nr + n_list) * 4, hipMemcpyHostToDevice, s));
-    if (merged) launch_miller_acc(pb, false, n_list, sl.d_list.p + 2 * (size_t)nr, s);
-    launch_group_reduce(pb, sl.d_list.p, sl.d_list.p, true, nr, sl.d_S.p, sl.d_F.p, s);
+    HIPCHK(hipMemcpyAsync(sl.d_list.p, hl, words * 4, hipMemcpyHostToDevice, s));
+    PipelineBuffers pr = pb;
+    pr.n_chunks = nc;
+    pr.chunk_first = sl.d_list.p + 4 * (size_t)nr;
+    pr.chunk_items = sl.d_list.p + 4 * (size_t)nr + rfirst.size();
+    launch_miller_acc(pr, false, s);
+    launch_group_reduce(pr, sl.d_list.p, sl.d_list.p + 2 * (size_t)nr, nr, sl.d_S.p, sl.d_F.p, s);
     launch_group_check(sl.d_S.p, sl.d_F.p, nr, sl.d_ok.p, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, nr, hipMemcpyDeviceToHost, s));
@@ -638,6 +671,7 @@ void finish_call(Call* c) {
     local.batch_sigs_success += c->sst[k].batch_sigs_success;
     local.unique_messages += c->sst[k].unique_messages;
     local.pairing_units += c->sst[k].pairing_units;
+    local.miller_chunks += c->sst[k].miller_chunks;
     if (c->rc[k] != BLSGPU_OK && c->rc[k] != BLSGPU_DEVICE_ERROR) status = c->rc[k];
   }
   local.devices_used = (uint32_t)c->shards.size();
@@ -909,6 +943,9 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
     ctx->opt.max_devices = value;
   } else if (k == "dedupe") {
     ctx->opt.dedupe = value != 0;
+  } else if (k == "miller_k") {
+    if (value < 1 || value > 64) return BLSGPU_ERR_ARGS;
+    ctx->opt.miller_k = value;
   } else {
     return BLSGPU_ERR_ARGS;
   }

@@ -69,6 +69,7 @@ class Stats(ctypes.Structure):
         ("stage_ms", ctypes.c_double * 8),
         ("unique_messages", ctypes.c_uint32),
         ("pairing_units", ctypes.c_uint32),
+        ("miller_chunks", ctypes.c_uint32),
     ]
 
 

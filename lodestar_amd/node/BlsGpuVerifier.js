@@ -21,13 +21,30 @@
  *     (state-transition/src/cache/pubkeyCache.ts:56-77) -- GPU aggregation, no main-thread
  *     PublicKey.aggregate (utils.ts:5-16);
  *   - an object registered with registerPubkey(obj, index) (a blst PublicKey, mapped by identity);
- *   - 96 uncompressed affine bytes (Uint8Array), or an object with toBytes() returning them -- what the
- *     pool sends to its workers today (index.ts:160); only for single sets.
- * A submission is in table mode when all its sets are indexed, in bytes mode otherwise; a flush that mixes
- * both is split into one submission per mode.
+ *   - any PublicKey-like object with toBytes() (96 uncompressed affine bytes, PointFormat.uncompressed),
+ *     or those 96 bytes as a Uint8Array -- what the pool sends its workers today (index.ts:160).  Aggregate
+ *     sets of such keys (the gossip attestation call, attestation.ts:131-138) are aggregated on the GPU
+ *     from the per-key bytes (bytes-aggregate mode), so no caller needs a registration pass.
+ * A job is in table mode when all its keys are indexed, in bytes mode otherwise; a flush that mixes both
+ * is split into one submission per mode.
+ *
+ * Metrics: the pool's blsThreadPool.* / bls.* series (metrics/metrics/lodestar.ts:382-458) are fed with the
+ * GPU as the worker (workerId = "gpu"): jobsWorkerTime, timePerSigSet, jobWaitTime, queueLength,
+ * totalJobsGroupsStarted, totalJobsStarted, totalSigSetsStarted, latencyToWorker, latencyFromWorker,
+ * successJobsSignatureSetsCount, errorJobsSignatureSetsCount, batchRetries, batchSigsSuccess,
+ * mainThreadDurationInThreadPool, aggregatedPubkeys.
+ *
+ * Also exported: BlsGpuSingleThreadVerifier (chain/bls/singleThread.ts:7-40 semantics: every call verified
+ * on its own, immediately, with the maybe-batch rule), verifySignatureSet (state-transition
+ * signatureSets.ts:24-38: Signature.verify / verifyAggregate), and the spec-conformance entry points
+ * fastAggregateVerify / ethFastAggregateVerify (beacon-node/test/spec/general/bls.ts: untrusted keys
+ * through KeyValidate, any error -> false).
  */
 const path = require("path");
 
+// Concurrent submissions run on separate runtime slots (HIP streams); HIP reads the hardware-queue count once,
+// at its first call (blsgpu_init), so the loader sets it unless the launcher already did (DESIGN.md).
+if (!process.env.GPU_MAX_HW_QUEUES) process.env.GPU_MAX_HW_QUEUES = "8";
 const addon = require(path.join(__dirname, "blsgpu_napi.node"));
 
 const MAX_BUFFERED_SIGS = 32; // multithread/index.ts:48
@@ -70,7 +87,10 @@ class BlsGpuVerifier {
     this.queuedTimer = null;
     this.inflight = new Set();
     this.pkIndexOf = new WeakMap();
-    this.stats = {submissions: 0, jobs: 0, sets: 0, groups: 0, batchRetries: 0, batchSigsSuccess: 0};
+    this.stats = {submissions: 0, jobs: 0, sets: 0, groups: 0, batchRetries: 0, batchSigsSuccess: 0, uniqueMessages: 0};
+    this.queueLength = 0; // submissions on the device (blsThreadPool.queueLength)
+    const m = this.metrics && this.metrics.blsThreadPool;
+    if (m && m.queueLength && m.queueLength.addCollect) m.queueLength.addCollect(() => m.queueLength.set(this.queueLength));
   }
 
   /** index2pubkey sync: entries [firstIndex, firstIndex + n) as 96-byte uncompressed affine encodings. */
@@ -99,7 +119,11 @@ class BlsGpuVerifier {
       for (const s of sets) if (s.type === SignatureSetType.aggregate) n += s.pubkeys.length;
       this.metrics.bls.aggregatedPubkeys.inc(n);
     }
+    // the pool path chunks the call into jobs and ANDs their results: no jobs -> "Empty results array"
+    // (multithread/index.ts:169-171); the main-thread path throws "Empty signature set" (maybeBatch.ts:29-31)
+    if (sets.length === 0) throw new Error(opts.verifyOnMainThread ? "Empty signature set" : "Empty results array");
     const job = this.encodeJob(sets, opts);
+    job.addedTimeMs = Date.now();
     const code = await new Promise((resolve, reject) => {
       job.resolve = resolve;
       job.reject = reject;
@@ -115,6 +139,7 @@ class BlsGpuVerifier {
         }
       } else if (opts.verifyOnMainThread) {
         // latency-critical (block proposal, interface.ts:8-17): no buffering at all
+        job.mainThread = true;
         this.dispatch([job]);
       } else {
         this.queued.push(job);
@@ -162,10 +187,14 @@ class BlsGpuVerifier {
     if (pk instanceof Uint8Array) return {bytes: pk};
     if (pk && typeof pk === "object") {
       const idx = this.pkIndexOf.get(pk);
-      if (idx !== undefined) return {index: idx};
-      if (typeof pk.toBytes === "function") return {bytes: pk.toBytes()};
+      const ref = {};
+      if (idx !== undefined) ref.index = idx;
+      // keep the bytes too (when the object serializes), so a job mixing registered and plain keys can go
+      // in bytes-aggregate mode
+      if (typeof pk.toBytes === "function") ref.bytes = pk.toBytes();
+      if (ref.index !== undefined || ref.bytes !== undefined) return ref;
     }
-    throw new TypeError("BlsGpuVerifier: pubkey must be an index, a registered object or 96 bytes");
+    throw new TypeError("BlsGpuVerifier: pubkey must be an index, a registered object, a PublicKey or 96 bytes");
   }
 
   encodeJob(sets, opts) {
@@ -177,11 +206,10 @@ class BlsGpuVerifier {
       enc.push({refs, msg: s.signingRoot, sig: s.signature, aggregate: s.type === SignatureSetType.aggregate});
     }
     if (!allIndexed) {
-      for (const e of enc) {
-        if (e.aggregate || e.refs.length !== 1 || e.refs[0].bytes === undefined || e.refs[0].bytes.length !== 96) {
-          throw new TypeError("BlsGpuVerifier: aggregate sets need indexed pubkeys; byte pubkeys must be 96-byte uncompressed");
-        }
-      }
+      for (const e of enc)
+        for (const r of e.refs)
+          if (r.bytes === undefined || r.bytes.length !== 96)
+            throw new TypeError("BlsGpuVerifier: pubkeys of a bytes-mode job must serialize to 96 uncompressed bytes");
     }
     return {sets: enc, table: allIndexed, batchable: !!opts.batchable};
   }
@@ -205,38 +233,48 @@ class BlsGpuVerifier {
     const msgs = new Uint8Array(32 * nSets);
     const sigs = new Uint8Array(SIG_STRIDE * nSets);
     const sigLen = new Uint32Array(nSets);
-    const req = {jobFirstSet, jobFlags, msgs, sigs, sigLen, sigStride: SIG_STRIDE, seed: this.seed};
-    let setPkFirst, pkIndex, pkBytes;
+    const setPkFirst = new Uint32Array(nSets + 1);
+    const req = {jobFirstSet, jobFlags, msgs, sigs, sigLen, sigStride: SIG_STRIDE, seed: this.seed, setPkFirst};
+    let pkIndex, pkBytes;
     if (tableMode) {
-      setPkFirst = req.setPkFirst = new Uint32Array(nSets + 1);
       pkIndex = req.pkIndex = new Uint32Array(Math.max(nPk, 1));
     } else {
-      pkBytes = req.pkBytes = new Uint8Array(96 * nSets);
+      pkBytes = req.pkBytes = new Uint8Array(Math.max(96 * nPk, 96));  // bytes-aggregate mode
     }
     let i = 0;
     let k = 0;
+    const now = Date.now();
+    const m = this.metrics && this.metrics.blsThreadPool;
     jobs.forEach((j, ji) => {
       jobFirstSet[ji] = i;
       jobFlags[ji] = j.batchable ? 1 : 0;
+      if (m && m.jobWaitTime && j.addedTimeMs) m.jobWaitTime.observe((now - j.addedTimeMs) / 1000);
       for (const s of j.sets) {
         msgs.set(s.msg.subarray(0, 32), 32 * i);
         const sl = s.sig.length;
         sigLen[i] = sl; // 96 / 192, anything else -> BLST_INVALID_SIZE for this job
         sigs.set(s.sig.subarray(0, Math.min(sl, SIG_STRIDE)), SIG_STRIDE * i);
-        if (tableMode) {
-          setPkFirst[i] = k;
-          for (const r of s.refs) pkIndex[k++] = r.index;
-        } else {
-          pkBytes.set(s.refs[0].bytes, 96 * i);
+        setPkFirst[i] = k;
+        for (const r of s.refs) {
+          if (tableMode) pkIndex[k] = r.index;
+          else pkBytes.set(r.bytes, 96 * k);
+          k++;
         }
         i++;
       }
     });
     jobFirstSet[jobs.length] = nSets;
-    if (tableMode) setPkFirst[nSets] = k;
-
+    setPkFirst[nSets] = k;
+    if (m) {
+      if (m.totalJobsGroupsStarted) m.totalJobsGroupsStarted.inc(1);
+      if (m.totalJobsStarted) m.totalJobsStarted.inc(jobs.length);
+      if (m.totalSigSetsStarted) m.totalSigSetsStarted.inc(nSets);
+    }
+    const submitNs = process.hrtime.bigint();
+    this.queueLength += 1;
     const p = addon.submit(this.ctx, req).then(
       (out) => {
+        this.queueLength -= 1;
         const st = this.stats;
         st.submissions++;
         st.jobs += jobs.length;
@@ -244,14 +282,29 @@ class BlsGpuVerifier {
         st.groups += out.groups;
         st.batchRetries += out.batchRetries;
         st.batchSigsSuccess += out.batchSigsSuccess;
-        const m = this.metrics && this.metrics.blsThreadPool;
+        st.uniqueMessages += out.uniqueMessages;
+        let okSets = 0;
+        let errSets = 0;
+        jobs.forEach((j, ji) => (out.results[ji] < 0 ? (errSets += j.sets.length) : (okSets += j.sets.length)));
         if (m) {
+          // the device is the worker: its time is the call's device phase; the rest is host <-> device latency
+          const totalSec = Number(process.hrtime.bigint() - submitNs) / 1e9;
+          const devSec = out.deviceMs / 1000;
+          if (m.jobsWorkerTime) m.jobsWorkerTime.inc({workerId: "gpu"}, devSec);
+          if (m.timePerSigSet && nSets) m.timePerSigSet.observe(devSec / nSets);
+          if (m.latencyToWorker) m.latencyToWorker.observe(Math.max(0, (totalSec - devSec) / 2));
+          if (m.latencyFromWorker) m.latencyFromWorker.observe(Math.max(0, (totalSec - devSec) / 2));
+          if (m.successJobsSignatureSetsCount) m.successJobsSignatureSetsCount.inc(okSets);
+          if (m.errorJobsSignatureSetsCount) m.errorJobsSignatureSetsCount.inc(errSets);
           if (m.batchRetries) m.batchRetries.inc(out.batchRetries);
           if (m.batchSigsSuccess) m.batchSigsSuccess.inc(out.batchSigsSuccess);
+          if (m.mainThreadDurationInThreadPool && jobs.some((j) => j.mainThread))
+            m.mainThreadDurationInThreadPool.observe(totalSec);
         }
         jobs.forEach((j, ji) => j.resolve(out.results[ji]));
       },
       (err) => {
+        this.queueLength -= 1;
         // call-level failure (device error, closed context): reject every job, never resolve false
         for (const j of jobs) j.reject(err.code === QUEUE_ABORTED ? new QueueError({code: QUEUE_ABORTED}) : err);
       }
@@ -261,4 +314,79 @@ class BlsGpuVerifier {
   }
 }
 
-module.exports = {BlsGpuVerifier, QueueError, SignatureSetType, MAX_BUFFERED_SIGS, MAX_BUFFER_WAIT_MS, addon};
+/**
+ * BlsSingleThreadVerifier semantics (chain/bls/singleThread.ts:7-40): every call is verified on its own,
+ * immediately (no buffering, no batching with other calls), by verifySignatureSetsMaybeBatch over its sets;
+ * errors reject.  Same device path: one non-batchable job per call.
+ */
+class BlsGpuSingleThreadVerifier extends BlsGpuVerifier {
+  async verifySignatureSets(sets) {
+    if (sets.length === 0) throw new Error("Empty signature set");
+    return super.verifySignatureSets(sets, {verifyOnMainThread: true});
+  }
+}
+
+/**
+ * verifySignatureSet (state-transition/src/util/signatureSets.ts:24-38): single -> Signature.verify,
+ * aggregate -> Signature.verifyAggregate (FastAggregateVerify over trusted keys).  Rejects like
+ * Signature.fromBytes(validate = true) on a malformed signature.
+ */
+async function verifySignatureSet(verifier, set) {
+  return verifier.verifySignatureSets([set], {verifyOnMainThread: true});
+}
+
+const G1_INFINITY_48 = (() => {
+  const b = new Uint8Array(48);
+  b[0] = 0xc0;
+  return b;
+})();
+const G2_INFINITY_96 = (() => {
+  const b = new Uint8Array(96);
+  b[0] = 0xc0;
+  return b;
+})();
+const sameBytes = (a, b) => a.length === b.length && a.every((x, i) => x === b[i]);
+
+/**
+ * fast_aggregate_verify of the spec runner (beacon-node/test/spec/general/bls.ts): untrusted 48-byte keys
+ * through KeyValidate (PublicKey.fromBytes(validate = true)), the signature through Signature.fromBytes
+ * (validate = true); any error -> false.
+ */
+async function fastAggregateVerify(verifier, pubkeys48, message, signature) {
+  if (pubkeys48.length === 0) return false; // EMPTY_AGGREGATE_ARRAY -> caught -> false
+  const flat = new Uint8Array(48 * pubkeys48.length);
+  pubkeys48.forEach((p, i) => flat.set(p.subarray(0, 48), 48 * i));
+  if (pubkeys48.some((p) => p.length !== 48)) return false;
+  const kv = addon.keyValidate(verifier.ctx, flat, 48);
+  if (kv.status.some((s) => s !== 0)) return false;
+  const keys = [];
+  for (let i = 0; i < pubkeys48.length; i++) keys.push(kv.pk96.subarray(96 * i, 96 * i + 96));
+  try {
+    return await verifier.verifySignatureSets(
+      [{type: SignatureSetType.aggregate, pubkeys: keys, signingRoot: message, signature}],
+      {verifyOnMainThread: true}
+    );
+  } catch (e) {
+    return false;
+  }
+}
+
+/** eth_fast_aggregate_verify (spec runner): no keys + infinity signature -> true; an infinity key -> false. */
+async function ethFastAggregateVerify(verifier, pubkeys48, message, signature) {
+  if (pubkeys48.length === 0 && sameBytes(signature, G2_INFINITY_96)) return true;
+  if (pubkeys48.some((p) => sameBytes(p, G1_INFINITY_48))) return false;
+  return fastAggregateVerify(verifier, pubkeys48, message, signature);
+}
+
+module.exports = {
+  BlsGpuVerifier,
+  BlsGpuSingleThreadVerifier,
+  verifySignatureSet,
+  fastAggregateVerify,
+  ethFastAggregateVerify,
+  QueueError,
+  SignatureSetType,
+  MAX_BUFFERED_SIGS,
+  MAX_BUFFER_WAIT_MS,
+  addon,
+};

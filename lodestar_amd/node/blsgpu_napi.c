@@ -18,6 +18,9 @@
  *     req = {jobFirstSet: Uint32Array, jobFlags?: Uint8Array, pkBytes?: Uint8Array,
  *            setPkFirst?: Uint32Array, pkIndex?: Uint32Array, msgs: Uint8Array, sigs: Uint8Array,
  *            sigLen: Uint32Array, sigStride: number, seed?: number}              blsgpu_submit
+ *     (pkBytes alone: one 96-B key per set; pkBytes + setPkFirst: bytes-aggregate; setPkFirst + pkIndex:
+ *      device table)
+ *   keyValidate(ctx, Uint8Array, pkLen) -> {pk96, status}        blsgpu_key_validate (synchronous)
  */
 #define NAPI_VERSION 6
 #include <node_api.h>
@@ -266,6 +269,8 @@ static void settle_on_main(napi_env env, napi_value js_cb, void* context, void* 
       set_num(env, out, "batchSigsSuccess", c->stats.batch_sigs_success);
       set_num(env, out, "devicesUsed", c->stats.devices_used);
       set_num(env, out, "deviceMs", c->stats.device_ms);
+      set_num(env, out, "uniqueMessages", c->stats.unique_messages);
+      set_num(env, out, "pairingUnits", c->stats.pairing_units);
       napi_resolve_deferred(env, c->deferred, out);
     }
   }
@@ -314,8 +319,9 @@ static napi_value Submit(napi_env env, napi_callback_info info) {
   /* shape checks on the host before anything reaches the device */
   int ok = ((const uint32_t*)jfs)[n_jobs] == n_sets && n_msgs == 32ull * n_sets &&
            n_sigs >= (size_t)stride * n_sets && (!flags || n_flags == n_jobs);
-  if (pkb) ok = ok && n_pkb == 96ull * n_sets;
-  else ok = ok && spf && n_spf == n_sets + 1ull && ((const uint32_t*)spf)[n_sets] <= n_pki;
+  if (pkb && !spf) ok = ok && n_pkb == 96ull * n_sets;  /* one key per set */
+  else if (pkb) ok = ok && n_spf == n_sets + 1ull && 96ull * ((const uint32_t*)spf)[n_sets] <= n_pkb;  /* bytes aggregate */
+  else ok = ok && spf && n_spf == n_sets + 1ull && ((const uint32_t*)spf)[n_sets] <= n_pki;  /* device table */
   if (!ok) {
     napi_throw_range_error(env, "BLSGPU_ERR_ARGS", "submit: inconsistent array sizes");
     return NULL;
@@ -352,6 +358,45 @@ static napi_value Submit(napi_env env, napi_callback_info info) {
   return promise;
 }
 
+/* keyValidate(ctx, Uint8Array pks, pkLen 48|96) -> {pk96: Uint8Array, status: Int8Array}  (synchronous) */
+static napi_value KeyValidate(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 3) {
+    napi_throw_type_error(env, NULL, "keyValidate(ctx, pks, pkLen)");
+    return NULL;
+  }
+  CtxBox* box = get_open_box(env, argv[0]);
+  if (!box) return NULL;
+  napi_typedarray_type t;
+  size_t len = 0;
+  void* data = NULL;
+  if (napi_get_typedarray_info(env, argv[1], &t, &len, &data, NULL, NULL) != napi_ok || t != napi_uint8_array) {
+    napi_throw_type_error(env, NULL, "keyValidate: pks must be a Uint8Array");
+    return NULL;
+  }
+  uint32_t pk_len = 0;
+  napi_get_value_uint32(env, argv[2], &pk_len);
+  if ((pk_len != 48 && pk_len != 96) || len % pk_len) {
+    napi_throw_range_error(env, "BLSGPU_ERR_ARGS", "keyValidate: pkLen must be 48 or 96 and divide the input");
+    return NULL;
+  }
+  uint32_t n = (uint32_t)(len / pk_len);
+  napi_value ab_pk, ab_st, pk96, st, out;
+  void *p_pk = NULL, *p_st = NULL;
+  CHECK(env, napi_create_arraybuffer(env, 96 * (size_t)n, &p_pk, &ab_pk));
+  CHECK(env, napi_create_arraybuffer(env, n ? n : 1, &p_st, &ab_st));
+  int rc = blsgpu_key_validate(box->ctx, n, (const uint8_t*)data, pk_len, pk_len, (uint8_t*)p_pk, (int8_t*)p_st);
+  if (rc != BLSGPU_OK) return throw_code(env, "blsgpu_key_validate", rc);
+  CHECK(env, napi_create_typedarray(env, napi_uint8_array, 96 * (size_t)n, ab_pk, 0, &pk96));
+  CHECK(env, napi_create_typedarray(env, napi_int8_array, n, ab_st, 0, &st));
+  CHECK(env, napi_create_object(env, &out));
+  napi_set_named_property(env, out, "pk96", pk96);
+  napi_set_named_property(env, out, "status", st);
+  return out;
+}
+
 static napi_value ModuleInit(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"init", NULL, Init, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
@@ -362,6 +407,7 @@ static napi_value ModuleInit(napi_env env, napi_value exports) {
       {"setOption", NULL, SetOption, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"codeName", NULL, CodeName, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"submit", NULL, Submit, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"keyValidate", NULL, KeyValidate, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   napi_value v;

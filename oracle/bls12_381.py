@@ -1087,6 +1087,46 @@ def verify_signature_sets_maybe_batch(sets, rng: SplitMix64 | None = None):
     return core_verify(pk, msg, signature_from_bytes(sig))
 
 
+def key_validate(pk_bytes: bytes):
+    """PublicKey.fromBytes(pk, validate=true) (reference state-transition/src/block/processDeposit.ts:56-64,
+    beacon-node/test/spec/general/bls.ts:121-124): decode (48 or 96 bytes), reject the identity and points
+    outside G1 (definitional [r]P == O).  Returns the affine point or raises BlstError."""
+    pt = g1_deserialize(bytes(pk_bytes))
+    if pt is None:
+        raise BlstError(BLST_PK_IS_INFINITY)
+    if g1_mul(pt, R) is not None:
+        raise BlstError(BLST_POINT_NOT_IN_GROUP)
+    return pt
+
+
+def fast_aggregate_verify(pks_bytes, msg: bytes, sig_bytes: bytes) -> bool:
+    """The spec runner's fast_aggregate_verify (reference beacon-node/test/spec/general/bls.ts:117-127):
+    Signature.fromBytes(validate) . verifyAggregate(PublicKey.fromBytes(validate) of each key); any error
+    -> false (EMPTY_AGGREGATE_ARRAY included)."""
+    try:
+        sig = signature_from_bytes(sig_bytes)
+        pks = [key_validate(p) for p in pks_bytes]
+        if not pks:
+            raise ValueError("EMPTY_AGGREGATE_ARRAY")
+        return core_verify(aggregate_pubkeys(pks), msg, sig)
+    except (BlstError, ValueError):
+        return False
+
+
+G1_INFINITY_COMPRESSED = bytes([0xC0]) + bytes(47)
+G2_INFINITY_COMPRESSED = bytes([0xC0]) + bytes(95)
+
+
+def eth_fast_aggregate_verify(pks_bytes, msg: bytes, sig_bytes: bytes) -> bool:
+    """eth_fast_aggregate_verify (reference spec/general/bls.ts:93-112): no keys + infinity signature ->
+    true; an infinity key -> false; otherwise fast_aggregate_verify."""
+    if not pks_bytes and bytes(sig_bytes) == G2_INFINITY_COMPRESSED:
+        return True
+    if any(bytes(p) == G1_INFINITY_COMPRESSED for p in pks_bytes):
+        return False
+    return fast_aggregate_verify(pks_bytes, msg, sig_bytes)
+
+
 def aggregate_pubkeys(pks):
     """bls.PublicKey.aggregate (reference chain/bls/utils.ts:11)."""
     if len(pks) == 0:

@@ -12,8 +12,35 @@ const fs = require("fs");
 const path = require("path");
 
 const ROOT = path.join(__dirname, "..", "..");
-const {BlsGpuVerifier} = require(path.join(ROOT, "lodestar_amd", "node", "BlsGpuVerifier.js"));
+const {
+  BlsGpuVerifier,
+  BlsGpuSingleThreadVerifier,
+  verifySignatureSet,
+  fastAggregateVerify,
+  ethFastAggregateVerify,
+} = require(path.join(ROOT, "lodestar_amd", "node", "BlsGpuVerifier.js"));
 const fx = JSON.parse(fs.readFileSync(path.join(ROOT, "tests", "golden", "verify_sets.json"), "utf8"));
+const fav = JSON.parse(fs.readFileSync(path.join(ROOT, "tests", "golden", "fav_cases.json"), "utf8"));
+
+// a PublicKey-like object (blst PublicKey.toBytes(PointFormat.uncompressed)), never registered
+const pkObject = (bytes) => ({toBytes: () => bytes});
+
+// metrics double: records every inc/observe/set by series name
+function fakeMetrics() {
+  const seen = {};
+  const series = (name) => ({
+    inc: (a, b) => (seen[name] = (seen[name] || 0) + (typeof a === "number" ? a : b === undefined ? 1 : b)),
+    observe: (v) => (seen[name] = (seen[name] || 0) + 1),
+    set: (v) => (seen[name] = v),
+    addCollect: (fn) => fn(),
+  });
+  const names = ["jobsWorkerTime", "successJobsSignatureSetsCount", "errorJobsSignatureSetsCount", "jobWaitTime",
+    "queueLength", "totalJobsGroupsStarted", "totalJobsStarted", "totalSigSetsStarted", "batchRetries",
+    "batchSigsSuccess", "latencyToWorker", "latencyFromWorker", "mainThreadDurationInThreadPool", "timePerSigSet"];
+  const blsThreadPool = {};
+  for (const n of names) blsThreadPool[n] = series(n);
+  return {seen, metrics: {blsThreadPool, bls: {aggregatedPubkeys: series("aggregatedPubkeys")}}};
+}
 
 const hex = (h) => Uint8Array.from(Buffer.from(h, "hex"));
 const keys = fx.keys.map((k) => hex(k.pk));
@@ -35,14 +62,17 @@ async function settle(p) {
   }
 }
 
-function expectOutcome(out, code, label) {
+function expectOutcome(out, code, label, mainThread = false) {
   if (code === 1 || code === 0) {
     assert.ok(!out.error, `${label}: unexpected rejection ${out.error && out.error.message}`);
     assert.strictEqual(out.value, code === 1, `${label}: expected ${code === 1}`);
   } else {
     assert.ok(out.error, `${label}: expected rejection (code ${code}), got ${out.value}`);
     const want = {8: "BLST_INVALID_SIZE", 1: "BLST_BAD_ENCODING", 2: "BLST_POINT_NOT_ON_CURVE",
-      3: "BLST_POINT_NOT_IN_GROUP", 9: "EMPTY_AGGREGATE_ARRAY", 10: "Empty signature set"}[-code];
+      3: "BLST_POINT_NOT_IN_GROUP", 9: "EMPTY_AGGREGATE_ARRAY",
+      // an empty call: the pool ANDs no job results (index.ts:169-171), the main thread path throws in
+      // verifySignatureSetsMaybeBatch (maybeBatch.ts:29-31)
+      10: mainThread ? "Empty signature set" : "Empty results array"}[-code];
     assert.ok(out.error.message.includes(want), `${label}: message "${out.error.message}" lacks ${want}`);
   }
 }
@@ -86,6 +116,72 @@ async function main() {
   assert.strictEqual(await v.verifySignatureSets(valid.slice(0, 3), {verifyOnMainThread: true}), true);
   console.log("ok verifyOnMainThread");
 
+  // aggregate sets of plain PublicKey objects (no registration): bytes-aggregate mode on the GPU -- the gossip
+  // attestation call (attestation.ts:131-138), every golden case
+  for (const c of fx.cases) {
+    const outs = await Promise.all(
+      c.jobs.map((j) =>
+        settle(
+          v.verifySignatureSets(
+            j.map((k) => {
+              const s = fx.sets[k];
+              return {type: "aggregate", pubkeys: s.pks.map((i) => pkObject(keys[i])), signingRoot: hex(s.msg),
+                signature: hex(s.sig)};
+            }),
+            {batchable: c.batchable}
+          )
+        )
+      )
+    );
+    outs.forEach((o, ji) => expectOutcome(o, c.expected[ji], `bytes-aggregate ${c.name} job ${ji}`));
+  }
+  console.log("ok aggregate sets of unregistered PublicKey objects (bytes-aggregate mode)");
+
+  // empty calls: the pool path rejects "Empty results array" (index.ts:169-171), the main-thread path
+  // "Empty signature set" (maybeBatch.ts:29-31)
+  const e1 = await settle(v.verifySignatureSets([], {batchable: true}));
+  assert.ok(e1.error && e1.error.message === "Empty results array", `empty pool call: ${e1.error}`);
+  const e2 = await settle(v.verifySignatureSets([], {verifyOnMainThread: true}));
+  assert.ok(e2.error && e2.error.message === "Empty signature set");
+  console.log("ok empty calls");
+
+  // 1,000-call gossip burst: one-pubkey aggregate sets of PublicKey objects, every 97th over a wrong root
+  {
+    const good = fx.sets.filter((s) => s.name.startsWith("single"));
+    const calls = [];
+    const want = [];
+    for (let i = 0; i < 1000; i++) {
+      const s = good[i % good.length];
+      const bad = i % 97 === 5;
+      const msg = hex(s.msg);
+      if (bad) msg[0] ^= 1;
+      calls.push(settle(v.verifySignatureSets(
+        [{type: "aggregate", pubkeys: [pkObject(keys[s.pks[0]])], signingRoot: msg, signature: hex(s.sig)}],
+        {batchable: true})));
+      want.push(!bad);
+    }
+    const t0 = Date.now();
+    const outs = await Promise.all(calls);
+    outs.forEach((o, i) => {
+      assert.ok(!o.error, `burst ${i}: ${o.error}`);
+      assert.strictEqual(o.value, want[i], `burst ${i}`);
+    });
+    console.log(`ok 1000-call gossip burst in ${Date.now() - t0} ms (${want.filter((x) => !x).length} false)`);
+  }
+
+  // verifySignatureSet (signatureSets.ts:24-38) and the spec runner's fast_aggregate_verify entry points
+  const agg = fx.sets.find((s) => s.name.startsWith("aggregate") && s.pks.length > 1);
+  assert.strictEqual(await verifySignatureSet(v, {type: "aggregate", pubkeys: agg.pks.map((i) => keys[i]),
+    signingRoot: hex(agg.msg), signature: hex(agg.sig)}), true);
+  for (const c of fav.cases) {
+    const pks = c.pubkeys.map(hex);
+    assert.strictEqual(await fastAggregateVerify(v, pks, hex(c.message), hex(c.signature)), c.fast_aggregate_verify,
+      `fast_aggregate_verify ${c.name}`);
+    assert.strictEqual(await ethFastAggregateVerify(v, pks, hex(c.message), hex(c.signature)),
+      c.eth_fast_aggregate_verify, `eth_fast_aggregate_verify ${c.name}`);
+  }
+  console.log(`ok verifySignatureSet + ${fav.cases.length} fast_aggregate_verify cases`);
+
   // close() rejects what is still buffered, and later calls
   const pending = settle(v.verifySignatureSets([valid[0]], {batchable: true}));
   await v.close();
@@ -94,6 +190,21 @@ async function main() {
   const after = await settle(v.verifySignatureSets([valid[0]]));
   assert.ok(after.error && after.error.message === "QUEUE_ERROR_QUEUE_ABORTED");
   console.log("ok close");
+
+  // BlsSingleThreadVerifier semantics + metrics of the pool series
+  const {seen, metrics} = fakeMetrics();
+  const st = new BlsGpuSingleThreadVerifier({seed: 7}, {metrics});
+  st.uploadPubkeys(0, Uint8Array.from(table));
+  const each = fx.cases.find((c) => c.name === "each_alone/plain");
+  const so = await Promise.all(each.jobs.map((j) => settle(st.verifySignatureSets(j.map((k) => toSet(fx.sets[k], true))))));
+  so.forEach((o, ji) => expectOutcome(o, each.expected[ji], `single-thread job ${ji}`, true));
+  const se = await settle(st.verifySignatureSets([]));
+  assert.ok(se.error && se.error.message === "Empty signature set");
+  for (const n of ["totalJobsStarted", "totalSigSetsStarted", "jobsWorkerTime", "timePerSigSet", "jobWaitTime",
+    "successJobsSignatureSetsCount", "errorJobsSignatureSetsCount", "latencyToWorker"])
+    assert.ok(seen[n] > 0, `metric ${n} not fed`);
+  await st.close();
+  console.log(`ok single-thread verifier, metrics ${JSON.stringify(seen)}`);
   console.log("ALL OK");
 }
 
