@@ -191,17 +191,22 @@ def build_c5(ctx, rank):
     return w, n, desc, int(round(desc["pubkeys_per_set"]))
 
 
-def stage_mults(n_sets, group_count, pubkeys_per_set):
+def stage_mults(n_sets, group_count, pubkeys_per_set, miller_k=2, n_messages=None):
     """Algorithmic work per stage in Montgomery multiplications (lodestar_amd/op_counts.json, counted on the
-    host build of the same device algorithm by tools/count_ops.py)."""
+    host build of the same device algorithm by tools/count_ops.py).  The Miller stage is priced as the kernels
+    run it: lines once per distinct message, accumulation per chunk of miller_k pairings."""
     with open(os.path.join(ROOT, "lodestar_amd", "op_counts.json")) as fh:
         oc = json.load(fh)
     per_set = {k: v["total"] for k, v in oc["per_set"].items()}
+    acc = oc["miller_acc_per_chunk"]
+    k = str(miller_k) if str(miller_k) in acc else "2"
+    per_set["miller_sets"] = (oc["miller_lines_per_message"] * (n_messages or n_sets) / n_sets
+                              + acc[k] / int(k))
     pgs = oc["per_group_per_set"]
     pgf = oc["per_group_fixed"]
     mults = {
         "sig_decode": per_set["sig_decode"] * n_sets,
-        "hash_to_g2": per_set["hash_to_g2"] * n_sets,
+        "hash_to_g2": per_set["hash_to_g2"] * (n_messages or n_sets),
         "pk_aggregate": oc["pk_aggregate_per_pubkey"] * n_sets * pubkeys_per_set if pubkeys_per_set > 1 else 0.0,
         "pk_finish": per_set["pk_finish"] * n_sets,
         "sig_scale": per_set["sig_scale"] * n_sets,
@@ -212,11 +217,11 @@ def stage_mults(n_sets, group_count, pubkeys_per_set):
     return mults, oc["products_per_mul"]
 
 
-def roofline(stage_ms_avg, n_sets, group_count, pubkeys_per_set, sets_per_s):
+def roofline(stage_ms_avg, n_sets, group_count, pubkeys_per_set, sets_per_s, miller_k=2, n_messages=None):
     """Dominant kernel: algorithmic limb products per launch / its average duration (HIP events on its
     stream, isolated profiled pass) against the measured v_mad_u64_u32 peak.  `pipeline_frac` is the whole
     chip over the timed (pipelined) region: algorithmic products/s at the measured sets/s over the peak."""
-    mults, ppm = stage_mults(n_sets, group_count, pubkeys_per_set)
+    mults, ppm = stage_mults(n_sets, group_count, pubkeys_per_set, miller_k, n_messages)
     from lodestar_amd.native import STAGES, KERNEL_OF_STAGE
 
     best = max(range(len(STAGES)), key=lambda k: stage_ms_avg[k])
@@ -414,7 +419,8 @@ def main():
         for _ in range(2):
             stage_acc += np.array(step().stage_ms[:8])
         ctx.set_option("profile", 0)
-        out["roofline"] = roofline(stage_acc / 2, n_sets // n_dev, groups // n_dev, pk_per_set, value / n_gpus)
+        out["roofline"] = roofline(stage_acc / 2, n_sets // n_dev, groups // n_dev, pk_per_set, value / n_gpus,
+                                   args.miller_k, stats[-1].unique_messages // n_dev)
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(dict(call, pks_table=work["pks_table"]) if "pks_table" in work else call,
                                            expected)

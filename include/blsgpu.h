@@ -175,6 +175,8 @@ const char* blsgpu_code_name(int code);
  * op: 0 fp_mul(48,48->48) 1 sig_decode(192+len -> status,192) 2 hash_to_g2(32->192)
  *     3 miller(96,192->576) 4 final_exp(576->576) 5 g1_mul_u64(96,8->96) 6 g2_mul_u64(192,8->192)
  *     7 sign(sk32||msg32 -> 96 compressed) 8 sk_to_pk(sk32 -> 96 uncompressed)   (workload generation)
+ *     9 g2_mul_scalar_word(192,8 -> 192; out_stride >= 2880) 10 g1_mul_scalar_word(96,8 -> 96; >= 1440):
+ *       the batch scalar r = 2w + 1 - 2^64 of a scalar word w (regular signed window)
  * Returns BLSGPU_OK or an error. */
 int blsgpu_debug_op(blsgpu_ctx* ctx, int op, uint32_t n, const uint8_t* in, uint32_t in_stride,
                     uint8_t* out, uint32_t out_stride, int32_t* status);

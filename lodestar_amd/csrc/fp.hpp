@@ -339,7 +339,14 @@ BLS_HD fp fp_from_mont(const fp& a) {
   return fp_canon(fp_mul(a, one));
 }
 
-// Exponentiation by a public constant (left-to-right binary; wave-uniform branches).
+// Exponentiation by a public constant: left-to-right sliding window of width 4 over the odd powers
+// a, a^3, ..., a^15 (379-381-bit exponents: 378 squarings + ~79 multiplications + 8 for the table, against
+// 378 + ~228 for the binary method).  Every branch depends only on the public, wave-uniform exponent.  The
+// table is a private array indexed by the (uniform) window digit: the same window with the eight powers held
+// as separate named values across the product calls and picked by a switch produced wrong results on gfx950
+// in the STAGE_KERNEL translation units (hipcc 7.2; tests/test_gpu_* caught it), the array form and a
+// width-3 window are correct -- keep it this way.  BLS_BINARY_POW=1 restores the binary method.
+#if BLS_BINARY_POW
 BLS_HDNI fp fp_pow_words(const fp& a, const uint32_t* e, int nbits) {
   fp r = a;
   for (int i = nbits - 2; i >= 0; i--) {
@@ -348,6 +355,37 @@ BLS_HDNI fp fp_pow_words(const fp& a, const uint32_t* e, int nbits) {
   }
   return r;
 }
+#else
+BLS_HDNI fp fp_pow_words(const fp& a, const uint32_t* e, int nbits) {
+  fp tab[8];
+  const fp a2 = fp_sqr(a);
+  tab[0] = a;
+  for (int k = 1; k < 8; k++) tab[k] = fp_mul(tab[k - 1], a2);
+  fp r = a;
+  bool started = false;
+  int i = nbits - 1;
+  while (i >= 0) {
+    if (!((e[i >> 5] >> (i & 31)) & 1u)) {
+      r = fp_sqr(r);
+      i--;
+      continue;
+    }
+    int j = i - 3 < 0 ? 0 : i - 3;
+    while (!((e[j >> 5] >> (j & 31)) & 1u)) j++;
+    uint32_t d = 0;
+    for (int k = i; k >= j; k--) d = (d << 1) | ((e[k >> 5] >> (k & 31)) & 1u);
+    if (started) {
+      for (int k = i; k >= j; k--) r = fp_sqr(r);
+      r = fp_mul(r, tab[d >> 1]);
+    } else {
+      r = tab[d >> 1];
+      started = true;
+    }
+    i = j - 1;
+  }
+  return r;
+}
+#endif
 
 BLS_HD fp fp_inv(const fp& a) { return fp_pow_words(a, EXP_P_MINUS_2, 381); }   // 0 -> 0
 BLS_HD fp fp_pow_p34(const fp& a) { return fp_pow_words(a, EXP_P_MINUS_3_DIV_4, 379); }

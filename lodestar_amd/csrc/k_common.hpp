@@ -130,6 +130,59 @@ __device__ jac<F> jac_mul_u64_j(const jac<F>& P, uint64_t k) {
   return r;
 }
 
+// [r]P for the batch scalar encoded by the 64-bit word w (runtime.cpp `scalar words`): r = sum_i d_i 16^i with
+// the 16 odd digits d_i = 2 nibble_i(w) - 15 in {-15, ..., 15}, i.e. r = 2w + 1 - 2^64 -- a bijection between
+// the 2^64 words and 2^64 distinct odd scalars, so the random linear combination keeps blst's 2^-64
+// soundness.  Regular signed window: every lane runs the same 61 doublings and 22 additions (no
+// data-dependent branch, unlike double-and-add with a lane-varying scalar); the table of odd multiples
+// P, 3P, ..., 15P lives in HBM (SoA, tab[(e * 3 * WF + word) * n + i], WF = words of one coordinate).
+template <class F>
+__device__ __forceinline__ void tab_st(uint32_t* tab, uint32_t n, uint32_t i, int e, const jac<F>& v) {
+  constexpr int WF = sizeof(F) / 4;
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+  for (int w = 0; w < 3 * WF; w++) tab[((size_t)e * 3 * WF + w) * n + i] = s[w];
+}
+template <class F>
+__device__ __forceinline__ jac<F> tab_ld(const uint32_t* tab, uint32_t n, uint32_t i, int e) {
+  constexpr int WF = sizeof(F) / 4;
+  jac<F> v;
+  uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+  for (int w = 0; w < 3 * WF; w++) d[w] = tab[((size_t)e * 3 * WF + w) * n + i];
+  return v;
+}
+template <class F>
+__device__ jac<F> jac_mul_scalar_word(const jac<F>& P, uint64_t w, uint32_t* tab, uint32_t n, uint32_t i) {
+  const jac<F> P2 = jac_dbl(P);
+  jac<F> t = P;
+  tab_st(tab, n, i, 0, t);
+#pragma unroll 1
+  for (int e = 1; e < 8; e++) {
+    t = jac_add(t, P2);
+    tab_st(tab, n, i, e, t);
+  }
+  auto digit = [&](int k, bool& neg) {
+    const int nib = (int)((w >> (4 * k)) & 15u);
+    const int d = 2 * nib - 15;
+    neg = d < 0;
+    return (d < 0 ? -d : d) >> 1;  // table entry of |d| = 2e + 1
+  };
+  bool neg;
+  int e = digit(15, neg);
+  jac<F> r = tab_ld<F>(tab, n, i, e);
+  if (neg) r = jac_neg(r);
+#pragma unroll 1
+  for (int k = 14; k >= 0; k--) {
+    r = jac_dbl(jac_dbl(jac_dbl(jac_dbl(r))));
+    e = digit(k, neg);
+    jac<F> q = tab_ld<F>(tab, n, i, e);
+    if (neg) q = jac_neg(q);
+    r = jac_add(r, q);
+  }
+  return r;
+}
+
 // [k]P for a multi-word scalar (little-endian 32-bit words), used by the workload-generation ops
 template <class F>
 __device__ jac<F> jac_mul_words(const jac<F>& P, const uint32_t* k, int nw) {

@@ -111,6 +111,24 @@ __global__ __launch_bounds__(WAVE) void k_debug_op(int op, uint32_t n, const uin
       if (st == 0) g1a_to_be96(pk, o);
       break;
     }
+    case 9: {  // batch-scalar-word multiple of a G2 point: 192 B || word (8 B LE) -> 192 B (table after it)
+      uint64_t w = 0;
+      for (int j = 0; j < 8; j++) w |= (uint64_t)a[192 + j] << (8 * j);
+      g2a r;
+      uint32_t* tab = reinterpret_cast<uint32_t*>(o + 192);
+      st = jac_to_aff(jac_mul_scalar_word(jac_from_aff(dbg_load_g2(a)), w, tab, 1, 0), r) ? 0 : -1;
+      if (st == 0) g2a_to_be192(r, o);
+      break;
+    }
+    case 10: {  // the same in G1: 96 B || word -> 96 B (table after it)
+      uint64_t w = 0;
+      for (int j = 0; j < 8; j++) w |= (uint64_t)a[96 + j] << (8 * j);
+      g1a r;
+      uint32_t* tab = reinterpret_cast<uint32_t*>(o + 96);
+      st = jac_to_aff(jac_mul_scalar_word(jac_from_aff(dbg_load_g1(a)), w, tab, 1, 0), r) ? 0 : -1;
+      if (st == 0) g1a_to_be96(r, o);
+      break;
+    }
     default:
       st = -2;
   }

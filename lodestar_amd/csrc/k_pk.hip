@@ -130,8 +130,8 @@ STAGE_KERNEL void k_pk_finish(PipelineBuffers b, uint32_t n_sets, int8_t* pk_sta
   out.x = fp_zero();
   out.y = fp_zero();
   if (st == BLS_OK) {
-    uint64_t r = b.scalars[i];
-    g1j R = (r == 1) ? P : jac_mul_u64_j(P, r);
+    const uint64_t w = b.scalars[i];  // batch scalar word, 0 = r = 1 (CoreVerify)
+    g1j R = (w == 0) ? P : jac_mul_scalar_word(P, w, b.scal_tab, b.n, i);
     if (!jac_to_aff(R, out)) st = BLS_PK_IS_INFINITY;
   }
   st_g1a(b.pk_aff, b.n, i, out);

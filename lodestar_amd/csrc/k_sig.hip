@@ -22,14 +22,15 @@ STAGE_KERNEL void k_sig_decode(PipelineBuffers b, uint32_t n_sets) {
   b.status[i] = (int8_t)st;
 }
 
+// r_i sig_i with the batch scalar word (0 = r = 1, CoreVerify); the signed-window table goes to b.scal_tab.
 STAGE_KERNEL void k_sig_scale(PipelineBuffers b, uint32_t n_sets) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets) return;
   g2j R = jac_infinity<fp2>();
   if (b.status[i] == BLS_OK && !(b.flags[i] & SF_SIG_INF)) {
-    g2a s = ld_g2a(b.sig_aff, b.n, i);
-    uint64_t r = b.scalars[i];
-    R = (r == 1) ? jac_from_aff(s) : jac_mul_u64(s, r);
+    const g2a s = ld_g2a(b.sig_aff, b.n, i);
+    const uint64_t w = b.scalars[i];
+    R = (w == 0) ? jac_from_aff(s) : jac_mul_scalar_word(jac_from_aff(s), w, b.scal_tab, b.n, i);
   }
   st_g2j(b.rsig, b.n, i, R);
 }

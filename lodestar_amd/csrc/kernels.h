@@ -34,7 +34,8 @@ struct PipelineBuffers {
   const uint32_t* pk_index;
   const uint32_t* pk_table;  // AoS W_PKTAB words per key
   uint32_t pk_table_n;
-  const uint64_t* scalars;
+  const uint64_t* scalars;  // batch scalar words (k_common.hpp jac_mul_scalar_word), 0 = r = 1
+  uint32_t* scal_tab;       // signed-window tables: 8 x W_G2J words per set (SoA, stride n)
   const uint32_t* job_first_set;  // [n_jobs + 1], shard-relative
   uint32_t n_jobs;
   // messages, deduplicated per call: set i signs umsgs[msg_idx[i]]

@@ -307,8 +307,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       }
       if (!batchable) {
         group_jobs.push_back({j, j + 1});
-        // single-set non-batchable job: CoreVerify (r = 1); multi-set: random linear combination
-        for (uint32_t i = a; i < e; i++) scal[i] = (e - a == 1) ? 1ull : splitmix64_at(seed, s0 + i);
+        // single-set non-batchable job: CoreVerify (r = 1, scalar word 0); multi-set: random linear combination
+        for (uint32_t i = a; i < e; i++) scal[i] = (e - a == 1) ? 0ull : splitmix64_at(seed, s0 + i);
         open = false;
         continue;
       }
@@ -459,7 +459,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   sl.d_S.ensure((size_t)W_G2J * max_ranges);
   sl.d_F.ensure((size_t)W_FP12 * max_ranges);
   // work area: per set sig_aff, pk_jac, pk_aff, rsig, f_set (+ per unit unit_p, f_unit), per message h_aff
-  const size_t per_set = W_G2A + W_G1J + W_G1A + W_G2J + W_FP12 + (merged ? W_G1A : 0);
+  const size_t per_set = W_G2A + W_G1J + W_G1A + W_G2J + W_FP12 + 8 * W_G2J + (merged ? W_G1A : 0);
   sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * W_G2A);
   sl.d_lines.ensure((size_t)nm * kMillerLineWords);
   hipStream_t s = sl.stream;
@@ -495,6 +495,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.pk_aff = w; w += (size_t)stride * W_G1A;
   pb.rsig = w; w += (size_t)stride * W_G2J;
   pb.f_chunk = w; w += (size_t)stride * W_FP12;
+  pb.scal_tab = w; w += (size_t)stride * 8 * W_G2J;
   if (merged) {
     pb.unit_p = w; w += (size_t)stride * W_G1A;
   }

@@ -56,6 +56,22 @@ static fp12 load12(const uint8_t* b) {
   return f;
 }
 
+// the device's regular signed-window scalar multiplication (k_common.hpp jac_mul_scalar_word), host table
+template <class F>
+static jac<F> emu_mul_scalar_word(const jac<F>& P, uint64_t w) {
+  jac<F> tab[8];
+  const jac<F> P2 = jac_dbl(P);
+  tab[0] = P;
+  for (int e = 1; e < 8; e++) tab[e] = jac_add(tab[e - 1], P2);
+  auto pick = [&](int k) {
+    const int d = 2 * (int)((w >> (4 * k)) & 15u) - 15;
+    jac<F> q = tab[(d < 0 ? -d : d) >> 1];
+    return d < 0 ? jac_neg(q) : q;
+  };
+  jac<F> r = pick(15);
+  for (int k = 14; k >= 0; k--) r = jac_add(jac_dbl(jac_dbl(jac_dbl(jac_dbl(r)))), pick(k));
+  return r;
+}
 extern "C" {
 #if defined(BLS_COUNT_OPS)
 void emu_count_reset() { bls_count_mul = bls_count_sqr = 0; }
@@ -66,6 +82,54 @@ void emu_stage_sig_scale(const uint8_t* sig192, uint64_t r) { (void)jac_mul_u64(
 void emu_stage_pk_finish(const uint8_t* pk96, uint64_t r) {
   g1a a;
   (void)jac_to_aff(jac_mul_u64(load_g1(pk96), r), a);
+}
+void emu_stage_sig_scale_w(const uint8_t* sig192, uint64_t w) { (void)emu_mul_scalar_word(jac_from_aff(load_g2(sig192)), w); }
+void emu_stage_pk_finish_w(const uint8_t* pk96, uint64_t w) {
+  g1a a;
+  (void)jac_to_aff(emu_mul_scalar_word(jac_from_aff(load_g1(pk96)), w), a);
+}
+// Miller stage as the kernels split it: lines per message (k_miller_lines), accumulation per chunk of k
+// pairings with shared squarings (k_miller_acc)
+void emu_stage_miller_lines(const uint8_t* q192) {
+  const g2a Q = load_g2(q192);
+  g2proj T;
+  T.x = Q.x;
+  T.y = Q.y;
+  T.z = fp2_one();
+  int bit = 62;
+  bool add_next = false;
+  for (int s = 0; s < MILLER_STEPS; s++) {
+    line3 L;
+    if (!add_next) {
+      miller_dbl_line(T, L);
+      add_next = (BLS_Z_ABS >> bit) & 1ull;
+      bit--;
+    } else {
+      miller_add_line(T, Q, L);
+      add_next = false;
+    }
+  }
+}
+void emu_stage_miller_acc(const uint8_t* pk96, const uint8_t* q192, int k) {
+  const g1a P = load_g1(pk96);
+  const g2a Q = load_g2(q192);
+  line3 L;
+  L.l0 = Q.x;
+  L.c1 = Q.y;
+  L.c4 = Q.x;
+  fp12 f = fp12_one();
+  int bit = 62;
+  bool add_next = false;
+  for (int s = 0; s < MILLER_STEPS; s++) {
+    if (!add_next && s != 0) f = fp12_sqr(f);
+    for (int j = 0; j < k; j++) f = fp12_mul_by_014(f, L.l0, fp2_mul_fp(L.c1, P.x), fp2_mul_fp(L.c4, P.y));
+    if (!add_next) {
+      add_next = (BLS_Z_ABS >> bit) & 1ull;
+      bit--;
+    } else {
+      add_next = false;
+    }
+  }
 }
 void emu_stage_group_sig_miller(const uint8_t* sig192, int n) {
   g2j S = jac_infinity<fp2>();

@@ -226,3 +226,27 @@ def test_verify_table_mode_aggregate(ctx):
     res, _ = ctx.verify_raw([0, 1, 2], sigs[:192], [96, 96], msgs[:64], set_pk_first=[0, 7, 7],
                             pk_index=list(range(7)), sig_stride=96)
     assert list(res) == [1, -9]
+
+
+def test_debug_scalar_word_mul():
+    """The batch scalar of word w is r = 2w + 1 - 2^64 (k_common.hpp jac_mul_scalar_word): G1 and G2 against
+    the oracle's plain scalar multiplication, including the extreme words."""
+    from lodestar_amd.native import Context
+
+    ctx = Context([0])
+    try:
+        rnd = random.Random(21)
+        words = [0, 1, 2**64 - 1, 2**63, 0x0F0F0F0F0F0F0F0F] + [rnd.getrandbits(64) for _ in range(11)]
+        P = bls.g1_mul(bls.G1_GEN, 987654321)
+        Q = bls.g2_mul(bls.G2_GEN, 123456789)
+        inp1 = b"".join(bls.g1_serialize(P) + w.to_bytes(8, "little") for w in words)
+        inp2 = b"".join(bls.g2_serialize(Q) + w.to_bytes(8, "little") for w in words)
+        o1, s1 = ctx.debug_op(10, inp1, 104, 1440)
+        o2, s2 = ctx.debug_op(9, inp2, 200, 2880)
+        assert (s1 == 0).all() and (s2 == 0).all()
+        for k, w in enumerate(words):
+            r = (2 * w + 1 - 2**64) % bls.R
+            assert o1[1440 * k: 1440 * k + 96] == bls.g1_serialize(bls.g1_mul(P, r))
+            assert o2[2880 * k: 2880 * k + 192] == bls.g2_serialize(bls.g2_mul(Q, r))
+    finally:
+        ctx.close()

@@ -30,8 +30,9 @@ def main():
     L = ctypes.CDLL(SO)
     L.emu_count_mul.restype = ctypes.c_ulonglong
     L.emu_count_sqr.restype = ctypes.c_ulonglong
-    L.emu_stage_sig_scale.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
-    L.emu_stage_pk_finish.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
+    L.emu_stage_sig_scale_w.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
+    L.emu_stage_pk_finish_w.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
+    L.emu_stage_miller_acc.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
     L.emu_g1_mul_u64.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
     L.emu_sig_decode.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
 
@@ -54,11 +55,12 @@ def main():
     m = iter(msgs * 4)
     stages["hash_to_g2"] = measure(lambda: L.emu_hash_to_g2(next(m), out), reps=8)
     s = iter(scal * 2)
-    stages["pk_finish"] = measure(lambda: L.emu_stage_pk_finish(g1b(pk), next(s)), reps=16)
+    stages["pk_finish"] = measure(lambda: L.emu_stage_pk_finish_w(g1b(pk), next(s)), reps=16)
     s = iter(scal * 2)
-    stages["sig_scale"] = measure(lambda: L.emu_stage_sig_scale(g2b(sig), next(s)), reps=16)
+    stages["sig_scale"] = measure(lambda: L.emu_stage_sig_scale_w(g2b(sig), next(s)), reps=16)
     H = bls.hash_to_g2(msgs[1])
-    stages["miller_sets"] = measure(lambda: L.emu_miller(g1b(pk), g2b(H), out))
+    lines = measure(lambda: L.emu_stage_miller_lines(g2b(H)))
+    acc = {k: measure(lambda: L.emu_stage_miller_acc(g1b(pk), g2b(H), k)) for k in (1, 2, 4, 8)}
     # per-group stages as a function of group size n: a + b n
     g0 = measure(lambda: L.emu_stage_group_sig_miller(g2b(sig), 0))
     g64 = measure(lambda: L.emu_stage_group_sig_miller(g2b(sig), 64))
@@ -75,8 +77,14 @@ def main():
         "per_group_fixed": {"group_sig_miller": tot(g0), "group_finish": tot(f0)},
         "per_group_per_set": {"group_sig_miller": (tot(g64) - tot(g0)) / 64, "group_finish": (tot(f64) - tot(f0)) / 64},
         "pk_aggregate_per_pubkey": (tot(a512) - tot(a0)) / 512,
+        # Miller stage split as the kernels run it: lines once per distinct message, accumulation per chunk of
+        # k pairings (shared squarings); per set = lines + acc_chunk[k] / k for distinct messages
+        "miller_lines_per_message": tot(lines),
+        "miller_acc_per_chunk": {str(k): tot(v) for k, v in acc.items()},
     }
-    per_set_total = sum(v["total"] for v in res["per_set"].values())
+    res["per_set"]["miller_sets"] = {"mul": None, "sqr": None,
+                                     "total": tot(lines) + tot(acc[2]) / 2, "note": "lines + acc_chunk[2] / 2"}
+    per_set_total = sum(v["total"] for v in res["per_set"].values())  # at the default miller_k = 2
     res["per_single_set_total"] = per_set_total
     path = os.path.join(ROOT, "lodestar_amd", "op_counts.json")
     with open(path, "w") as fh:
