@@ -137,7 +137,9 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
 /* Tunables: "group_sets" (sets per batch group before a new one opens, default 256), "slots" (runtime slots
  * per device, only grows, default 4), "max_devices" (devices one call may shard over, default all),
  * "dedupe" (message dedupe + same-message pairing, 0/1, default 1), "miller_k" (pairings per Miller
- * accumulator sharing its Fp12 squarings, 1..64, default 2), "profile" (per-stage kernel times in
+ * accumulator sharing its Fp12 squarings, 1..64, default 2), "merge_sets" (a runtime slot merges calls
+ * already queued on its device into one pipeline run of up to this many sets -- jobs and results stay per
+ * call -- default 65536, 0 = never), "profile" (per-stage kernel times in
  * blsgpu_stats.stage_ms, 0/1).  Applies to calls submitted afterwards. */
 int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value);
 

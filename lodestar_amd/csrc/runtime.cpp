@@ -149,6 +149,10 @@ struct Options {  // snapshot taken at the start of each call
   bool profile = false;
   bool dedupe = true;
   int64_t miller_k = 2;  // pairings per Miller accumulator (shared squarings)
+  int64_t merge_sets = 65536;  // queued calls a slot merges into one pipeline run (sets), 0 = never
+  bool same_run(const struct Options& o) const {
+    return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k;
+  }
 };
 
 // Splits item ranges into Miller chunks of <= k items: appends to first/items, returns [chunk_begin, end)
@@ -276,7 +280,7 @@ struct MsgIndex {
 
 // Runs one device's shard on one slot.  Writes job_result[job_begin..job_end).
 int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_t* job_result, uint64_t seed,
-              const Options& opt, uint32_t max_index, blsgpu_stats& st) {
+              const Options& opt, uint32_t max_index, blsgpu_stats& st, const uint64_t* scal_words = nullptr) {
   const uint32_t n = sh.set_end - sh.set_begin;
   const uint32_t nj = sh.job_end - sh.job_begin;
   if (nj == 0) return BLSGPU_OK;
@@ -322,6 +326,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       cur_sets += e - a;
     }
   }
+  if (scal_words) memcpy(scal.data(), scal_words, (size_t)n * 8);  // merged calls: each part's own seed
   auto job_sets = [&](uint32_t j) {
     const uint32_t gj = sh.job_begin + j;
     return std::make_pair(b.job_first_set[gj] - s0, b.job_first_set[gj + 1] - s0);
@@ -695,6 +700,109 @@ void finish_call(Call* c) {
   leave(ctx);
 }
 
+// pubkey mode of a batch: 0 table, 1 one key per set (bytes), 2 bytes aggregate
+inline int pk_mode(const blsgpu_batch& b) { return !b.pk_bytes ? 0 : (b.set_pk_first ? 2 : 1); }
+
+// Batch scalar words of a shard (shard-relative), the rule run_shard applies: single-set non-batchable jobs
+// use r = 1 (word 0, CoreVerify), every other set a SplitMix64 word of the call's seed.
+void shard_scalars(const blsgpu_batch& b, const Shard& sh, uint64_t seed, uint64_t* out) {
+  for (uint32_t j = sh.job_begin; j < sh.job_end; j++) {
+    const uint32_t a = b.job_first_set[j], e = b.job_first_set[j + 1];
+    const bool batchable = b.job_flags && (b.job_flags[j] & 1u);
+    for (uint32_t i = a; i < e; i++)
+      out[i - sh.set_begin] = (!batchable && e - a == 1) ? 0ull : splitmix64_at(seed, i);
+  }
+}
+
+// Several queued shards (of different calls) run as ONE pipeline: their inputs are concatenated into one
+// batch (jobs and results stay per call), so a launch fills the chip instead of one call's 16k-set share --
+// the device-side counterpart of the pool packing queued jobs into one worker request (prepareWork,
+// multithread/index.ts:386-401).  Jobs never interact, so every job's result is the one it gets alone.
+int run_merged(Device& d, Slot& sl, const std::vector<Task>& parts, std::vector<int>& rcs) {
+  const Call* c0 = parts[0].call;
+  const int mode = pk_mode(c0->b);
+  uint32_t n = 0, nj = 0, npk = 0, max_index = 0;
+  for (const Task& t : parts) {
+    const Shard& sh = t.call->shards[t.shard];
+    const blsgpu_batch& b = t.call->b;
+    n += sh.set_end - sh.set_begin;
+    nj += sh.job_end - sh.job_begin;
+    if (b.set_pk_first) npk += b.set_pk_first[sh.set_end] - b.set_pk_first[sh.set_begin];
+    max_index = std::max(max_index, t.call->max_index);
+  }
+  std::vector<uint32_t> jfs{0}, siglen, spf{0}, pki;
+  std::vector<uint8_t> flags, pkb, msgs, sigs;
+  std::vector<uint64_t> scal(n);
+  jfs.reserve(nj + 1);
+  siglen.reserve(n);
+  msgs.reserve((size_t)n * 32);
+  sigs.reserve((size_t)n * 192);
+  if (mode == 0) pki.reserve(npk);
+  if (mode == 1) pkb.reserve((size_t)n * 96);
+  if (mode == 2) pkb.reserve((size_t)npk * 96);
+  uint32_t so = 0;
+  for (const Task& t : parts) {
+    const Shard& sh = t.call->shards[t.shard];
+    const blsgpu_batch& b = t.call->b;
+    shard_scalars(b, sh, t.call->seed, scal.data() + so);
+    for (uint32_t j = sh.job_begin; j < sh.job_end; j++) {
+      jfs.push_back(so + b.job_first_set[j + 1] - sh.set_begin);
+      flags.push_back(b.job_flags ? b.job_flags[j] : 0);
+    }
+    for (uint32_t i = sh.set_begin; i < sh.set_end; i++) {
+      const uint32_t len = b.sig_len[i];
+      siglen.push_back(len);
+      const size_t at = sigs.size();
+      sigs.resize(at + 192, 0);
+      if (len == 96 || len == 192) memcpy(sigs.data() + at, b.sigs + (size_t)i * b.sig_stride, len);
+    }
+    msgs.insert(msgs.end(), b.msgs + (size_t)sh.set_begin * 32, b.msgs + (size_t)sh.set_end * 32);
+    if (mode == 1) {
+      pkb.insert(pkb.end(), b.pk_bytes + (size_t)sh.set_begin * 96, b.pk_bytes + (size_t)sh.set_end * 96);
+    } else {
+      const uint32_t k0 = b.set_pk_first[sh.set_begin];
+      for (uint32_t i = sh.set_begin; i < sh.set_end; i++) spf.push_back(spf.back() + b.set_pk_first[i + 1] - b.set_pk_first[i]);
+      if (mode == 0)
+        pki.insert(pki.end(), b.pk_index + k0, b.pk_index + b.set_pk_first[sh.set_end]);
+      else
+        pkb.insert(pkb.end(), b.pk_bytes + (size_t)k0 * 96, b.pk_bytes + (size_t)b.set_pk_first[sh.set_end] * 96);
+    }
+    so += sh.set_end - sh.set_begin;
+  }
+  blsgpu_batch mb{};
+  mb.n_sets = n;
+  mb.n_jobs = nj;
+  mb.job_first_set = jfs.data();
+  mb.job_flags = flags.data();
+  mb.pk_bytes = mode ? pkb.data() : nullptr;
+  mb.set_pk_first = mode == 1 ? nullptr : spf.data();
+  mb.pk_index = mode == 0 ? pki.data() : nullptr;
+  mb.msgs = msgs.data();
+  mb.sigs = sigs.data();
+  mb.sig_len = siglen.data();
+  mb.sig_stride = 192;
+  std::vector<int8_t> res(nj, 0);
+  blsgpu_stats st{};
+  const Shard all{0, nj, 0, n};
+  int rc;
+  try {
+    rc = run_shard(d, sl, mb, all, res.data(), c0->seed, c0->opt, max_index, st, scal.data());
+  } catch (...) {
+    rc = BLSGPU_DEVICE_ERROR;
+  }
+  uint32_t jo = 0;
+  for (size_t p = 0; p < parts.size(); p++) {
+    Call* c = parts[p].call;
+    const Shard& sh = c->shards[parts[p].shard];
+    for (uint32_t j = sh.job_begin; j < sh.job_end; j++)
+      c->job_result[j] = rc == BLSGPU_DEVICE_ERROR ? -BLSGPU_DEVICE_ERROR : res[jo++];
+    if (rc == BLSGPU_DEVICE_ERROR) jo += sh.job_end - sh.job_begin;
+    if (p == 0) c->sst[parts[p].shard] = st;  // the merged run's counters go to its first call
+    rcs[p] = rc;
+  }
+  return rc;
+}
+
 void run_task(Device& d, Slot& sl, const Task& t) {
   Call* c = t.call;
   const Shard& sh = c->shards[t.shard];
@@ -715,18 +823,49 @@ void run_task(Device& d, Slot& sl, const Task& t) {
   if (c->remaining.fetch_sub(1) == 1) finish_call(c);
 }
 
+inline uint32_t task_sets(const Task& t) {
+  const Shard& sh = t.call->shards[t.shard];
+  return sh.set_end - sh.set_begin;
+}
+
 void worker_loop(Device* d, Slot* sl) {
   (void)hipSetDevice(d->id);
   for (;;) {
-    Task t;
+    std::vector<Task> parts;
     {
       std::unique_lock<std::mutex> lk(d->q_mu);
       d->q_cv.wait(lk, [&] { return d->stop || !d->queue.empty(); });
       if (d->queue.empty()) return;  // stop requested and nothing left
-      t = d->queue.front();
+      parts.push_back(d->queue.front());
       d->queue.pop_front();
+      // merge further queued shards of compatible calls, up to merge_sets sets in total
+      const Call* c0 = parts[0].call;
+      uint32_t total = task_sets(parts[0]);
+      const int64_t cap = c0->opt.merge_sets;
+      while (!d->queue.empty() && cap > 0 && !(c0->ctx->closed)) {
+        const Task& nx = d->queue.front();
+        const Call* c = nx.call;
+        if ((int64_t)(total + task_sets(nx)) > cap || pk_mode(c->b) != pk_mode(c0->b) || !c->opt.same_run(c0->opt))
+          break;
+        total += task_sets(nx);
+        parts.push_back(nx);
+        d->queue.pop_front();
+      }
     }
-    run_task(*d, *sl, t);
+    if (parts.size() == 1) {
+      run_task(*d, *sl, parts[0]);
+      continue;
+    }
+    std::vector<int> rcs(parts.size(), BLSGPU_OK);
+    {
+      std::shared_lock<std::shared_mutex> tl(d->table_mu);
+      run_merged(*d, *sl, parts, rcs);
+    }
+    for (size_t p = 0; p < parts.size(); p++) {
+      Call* c = parts[p].call;
+      c->rc[parts[p].shard] = rcs[p];
+      if (c->remaining.fetch_sub(1) == 1) finish_call(c);
+    }
   }
 }
 
@@ -944,6 +1083,9 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
     ctx->opt.max_devices = value;
   } else if (k == "dedupe") {
     ctx->opt.dedupe = value != 0;
+  } else if (k == "merge_sets") {
+    if (value < 0) return BLSGPU_ERR_ARGS;
+    ctx->opt.merge_sets = value;
   } else if (k == "miller_k") {
     if (value < 1 || value > 64) return BLSGPU_ERR_ARGS;
     ctx->opt.miller_k = value;
