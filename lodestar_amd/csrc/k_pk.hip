@@ -11,9 +11,9 @@ __global__ __launch_bounds__(WAVE) void k_pk_aggregate(PipelineBuffers b, uint32
   __shared__ uint32_t red[WAVE * W_G1J];
   __shared__ uint32_t err_k[WAVE];
   __shared__ int32_t err_c[WAVE];
-  uint32_t set = blockIdx.x;
+  if (blockIdx.x >= n_sets) return;
+  const uint32_t set = b.agg_sets ? b.agg_sets[blockIdx.x] : blockIdx.x;
   uint32_t lane = threadIdx.x;
-  if (set >= n_sets) return;
   int8_t* agg_status = b.status + 2 * b.n;
   const uint32_t first = b.set_pk_first[set], last = b.set_pk_first[set + 1];
   g1j acc = jac_infinity<fp>();
@@ -93,11 +93,21 @@ __global__ __launch_bounds__(WAVE) void k_pk_aggregate(PipelineBuffers b, uint32
   if (lane == 0) st_g1j(b.pk_jac, b.n, set, acc);
 }
 
-// The set's (aggregated) public key as a Jacobian point + status.  Single-key bytes mode decodes pk_bytes.
+// The set's (aggregated) public key as a Jacobian point + status.  Single-key bytes mode decodes pk_bytes;
+// with pk_direct1 a one-key set of table / bytes-aggregate mode reads its key here (k_pk_aggregate skipped it:
+// the aggregate of one key is that key, an identity key aggregates to the identity).
 __device__ __forceinline__ int set_pubkey(const PipelineBuffers& b, uint32_t i, g1j& P) {
-  if (b.pk_bytes && !b.set_pk_first) {
+  const bool one = b.set_pk_first && b.pk_direct1 && b.set_pk_first[i + 1] - b.set_pk_first[i] == 1;
+  if (one && !b.pk_bytes) {
+    const uint32_t idx = b.pk_index[b.set_pk_first[i]];
+    if (idx >= b.pk_table_n) return BLS_DEVICE_ERROR;
+    P = jac_from_aff(ld_pktab(b.pk_table, idx));
+    return BLS_OK;
+  }
+  if (b.pk_bytes && (!b.set_pk_first || one)) {
     uint8_t raw[96];
-    const uint4* src = reinterpret_cast<const uint4*>(b.pk_bytes + (size_t)i * 96);
+    const uint32_t k = b.set_pk_first ? b.set_pk_first[i] : i;
+    const uint4* src = reinterpret_cast<const uint4*>(b.pk_bytes + (size_t)k * 96);
 #pragma unroll
     for (int k = 0; k < 6; k++) {
       uint4 v = src[k];
@@ -232,6 +242,7 @@ __global__ __launch_bounds__(WAVE) void k_pk_table_fill(const uint8_t* pk96, uin
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
 void launch_pk_aggregate(const PipelineBuffers& b, uint32_t n, hipStream_t s) {
+  if (b.agg_sets) n = b.n_agg;
   if (n) hipLaunchKernelGGL(k_pk_aggregate, dim3(n), dim3(WAVE), 0, s, b, n);
 }
 void launch_pk_finish(const PipelineBuffers& b, uint32_t n, hipStream_t s) {

@@ -34,6 +34,11 @@ struct PipelineBuffers {
   const uint32_t* pk_index;
   const uint32_t* pk_table;  // AoS W_PKTAB words per key
   uint32_t pk_table_n;
+  // aggregation list: k_pk_aggregate runs one wave per set agg_sets[0 .. n_agg) (all sets when null); with
+  // pk_direct1, a set of exactly one key skips it and k_pk_finish reads / decodes that key itself
+  const uint32_t* agg_sets;
+  uint32_t n_agg;
+  uint32_t pk_direct1;
   const uint64_t* scalars;  // batch scalar words (k_common.hpp jac_mul_scalar_word), 0 = r = 1
   uint32_t* scal_tab;       // signed-window tables: 8 x W_G2J words per set (SoA, stride n)
   const uint32_t* job_first_set;  // [n_jobs + 1], shard-relative

@@ -390,6 +390,11 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     g_chunks[2 * g + 1] = cr.second;
   }
   const uint32_t n_chunks = (uint32_t)chunk_first.size() - 1;
+  // sets that aggregate >= 2 keys (one wave each in k_pk_aggregate); one-key sets are read by k_pk_finish
+  std::vector<uint32_t> agg_sets;
+  if (table_mode || bytes_agg)
+    for (uint32_t i = 0; i < n; i++)
+      if (b.set_pk_first[s0 + i + 1] - b.set_pk_first[s0 + i] >= 2) agg_sets.push_back(i);
 
   // ---- stage inputs in the pinned arena and copy it to the device in one transfer ------------------------
   // arena (256-B aligned sections): scalars | job_first_set | sigs (192 B each) | sig_len | unique msgs |
@@ -401,7 +406,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
                o_ufirst = al256(o_franges + (size_t)std::max(ng0, 1u) * 8),
                o_usets = al256(o_ufirst + (size_t)(n_units + 1) * 4), o_umsgi = al256(o_usets + (size_t)unit_sets.size() * 4),
                o_cfirst = al256(o_umsgi + (size_t)n_units * 4), o_citems = al256(o_cfirst + (size_t)(n_chunks + 1) * 4),
-               o_pk = al256(o_citems + chunk_items.size() * 4);
+               o_agg = al256(o_citems + chunk_items.size() * 4), o_pk = al256(o_agg + agg_sets.size() * 4);
   size_t in_bytes;
   if (table_mode)
     in_bytes = al256(o_pk + (size_t)(n + 1) * 4) + (size_t)npk * 4;
@@ -437,6 +442,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   }
   memcpy(hin + o_cfirst, chunk_first.data(), chunk_first.size() * 4);
   memcpy(hin + o_citems, chunk_items.data(), chunk_items.size() * 4);
+  if (!agg_sets.empty()) memcpy(hin + o_agg, agg_sets.data(), agg_sets.size() * 4);
   if (merged) {
     memcpy(hin + o_ufirst, unit_first.data(), (size_t)(n_units + 1) * 4);
     memcpy(hin + o_usets, unit_sets.data(), unit_sets.size() * 4);
@@ -483,6 +489,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.pk_index = table_mode ? reinterpret_cast<uint32_t*>(din + o_pk2) : nullptr;
   pb.pk_table = d.table.p;
   pb.pk_table_n = d.table_n;
+  pb.agg_sets = reinterpret_cast<uint32_t*>(din + o_agg);
+  pb.n_agg = (uint32_t)agg_sets.size();
+  pb.pk_direct1 = 1;
   pb.scalars = reinterpret_cast<uint64_t*>(din + o_scal);
   pb.job_first_set = reinterpret_cast<uint32_t*>(din + o_jobs);
   pb.n_jobs = nj;
@@ -527,7 +536,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   mark(1);
   launch_hash_to_g2(pb, s);
   mark(2);
-  if (table_mode || bytes_agg) launch_pk_aggregate(pb, n, s);
+  if ((table_mode || bytes_agg) && pb.n_agg) launch_pk_aggregate(pb, n, s);
   mark(3);
   launch_pk_finish(pb, n, s);
   mark(4);
