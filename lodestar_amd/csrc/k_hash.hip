@@ -11,15 +11,10 @@ STAGE_KERNEL void k_hash_to_g2(PipelineBuffers b) {
   uint32_t w[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
 #pragma unroll
   for (int k = 0; k < 32; k++) msg[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-  g2j h = hash_to_g2_jac(msg);
-  g2a a;
-  bool ok = jac_to_aff(h, a);
-  if (!ok) {
-    a.x = fp2_zero();
-    a.y = fp2_zero();
-  }
-  st_g2a(b.h_aff, b.nm, u, a);
-  b.mflags[u] = ok ? 0 : MF_H_INF;
+  // Jacobian out; the affine conversion is batched over the messages (k_inv.hip k_h_affine)
+  const g2j h = hash_to_g2_jac(msg);
+  st_g2j(b.h_jac, b.nm, u, h);
+  st_fp(b.h_norm, b.nm, u, 0, fp2_norm(h.z));
 }
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }

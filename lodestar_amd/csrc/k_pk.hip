@@ -129,22 +129,22 @@ __device__ __forceinline__ int set_pubkey(const PipelineBuffers& b, uint32_t i, 
   return jac_is_inf(P) ? BLS_PK_IS_INFINITY : BLS_OK;
 }
 
-// r_i * pk_i -> affine.  pk statuses go to their own array (status[n, 2n)); the job mask gives them
-// precedence over signature statuses because the reference deserializes pubkeys first (worker.ts:39).
+// r_i * pk_i, Jacobian, in place of the aggregate in pk_jac (the affine conversion is batched, k_inv.hip
+// k_pk_affine, which also maps an infinite r_i pk_i to PK_IS_INFINITY).  pk statuses go to their own array
+// (status[n, 2n)); the job mask gives them precedence over signature statuses because the reference
+// deserializes pubkeys first (worker.ts:39).  A set with a pubkey error stores the identity (z = 0), which
+// the batch inversion skips.
 STAGE_KERNEL void k_pk_finish(PipelineBuffers b, uint32_t n_sets, int8_t* pk_status) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets) return;
   g1j P;
   int st = set_pubkey(b, i, P);
-  g1a out;
-  out.x = fp_zero();
-  out.y = fp_zero();
+  g1j R = jac_infinity<fp>();
   if (st == BLS_OK) {
     const uint64_t w = b.scalars[i];  // batch scalar word, 0 = r = 1 (CoreVerify)
-    g1j R = (w == 0) ? P : jac_mul_scalar_word(P, w, b.scal_tab, b.n, i);
-    if (!jac_to_aff(R, out)) st = BLS_PK_IS_INFINITY;
+    R = (w == 0) ? P : jac_mul_scalar_word(P, w, b.scal_tab, b.n, i);
   }
-  st_g1a(b.pk_aff, b.n, i, out);
+  st_g1j(b.pk_jac, b.n, i, R);
   pk_status[i] = (int8_t)st;
 }
 

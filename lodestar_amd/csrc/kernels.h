@@ -57,6 +57,9 @@ struct PipelineBuffers {
   // ---- intermediates
   uint32_t* sig_aff;  // W_G2A, per set
   uint32_t* h_aff;    // W_G2A, per message
+  uint32_t* h_jac;    // W_G2J, per message: H(m) before the batched affine conversion (k_inv.hip)
+  uint32_t* h_norm;   // W_FP, per message: N(z) of h_jac
+  uint32_t* inv_buf;  // W_FP, per max(set, message): batch inversion output (k_inv.hip)
   uint32_t* pk_jac;   // W_G1J, per set (aggregate)
   uint32_t* pk_aff;   // W_G1A, per set (r * pk, affine)
   uint32_t* rsig;     // W_G2J, per set
@@ -80,6 +83,10 @@ void launch_sig_decode(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s)
 void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s);  // over the unique messages
 void launch_pk_aggregate(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 void launch_pk_finish(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
+// batched affine conversions (Montgomery's simultaneous inversion, k_inv.hip): r_i pk_i -> pk_aff, H(m) -> h_aff
+void launch_batch_inv(const uint32_t* src, uint32_t src_stride, int w0, uint32_t* dst, uint32_t n, hipStream_t s);
+void launch_pk_affine(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
+void launch_h_affine(const PipelineBuffers& b, hipStream_t s);
 void launch_sig_scale(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 // per-job error status and the per-set include mask of the batch equation
 void launch_job_mask(const PipelineBuffers& b, hipStream_t s);

@@ -470,8 +470,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   sl.d_S.ensure((size_t)W_G2J * max_ranges);
   sl.d_F.ensure((size_t)W_FP12 * max_ranges);
   // work area: per set sig_aff, pk_jac, pk_aff, rsig, f_set (+ per unit unit_p, f_unit), per message h_aff
-  const size_t per_set = W_G2A + W_G1J + W_G1A + W_G2J + W_FP12 + 8 * W_G2J + (merged ? W_G1A : 0);
-  sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * W_G2A);
+  const size_t per_set = W_G2A + W_G1J + W_G1A + W_G2J + W_FP12 + 8 * W_G2J + W_FP + (merged ? W_G1A : 0);
+  sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * (W_G2A + W_G2J + W_FP));
   sl.d_lines.ensure((size_t)nm * kMillerLineWords);
   hipStream_t s = sl.stream;
   uint8_t* const din = sl.d_in.p;
@@ -516,7 +516,10 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.n_chunks = n_chunks;
   pb.chunk_first = reinterpret_cast<uint32_t*>(din + o_cfirst);
   pb.chunk_items = reinterpret_cast<uint32_t*>(din + o_citems);
-  pb.h_aff = w;
+  pb.inv_buf = w; w += (size_t)stride * W_FP;  // n_umsg <= n
+  pb.h_aff = w; w += (size_t)nm * W_G2A;
+  pb.h_jac = w; w += (size_t)nm * W_G2J;
+  pb.h_norm = w;
   pb.lines = sl.d_lines.p;
   uint8_t* const db = sl.d_bytes.p;
   pb.flags = db + ob_flags;
@@ -535,10 +538,12 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   launch_sig_decode(pb, n, s);
   mark(1);
   launch_hash_to_g2(pb, s);
+  launch_h_affine(pb, s);
   mark(2);
   if ((table_mode || bytes_agg) && pb.n_agg) launch_pk_aggregate(pb, n, s);
   mark(3);
   launch_pk_finish(pb, n, s);
+  launch_pk_affine(pb, n, s);
   mark(4);
   launch_sig_scale(pb, n, s);
   launch_job_mask(pb, s);
