@@ -231,22 +231,39 @@ BLS_HDNI g2j clear_cofactor_g2(const g2j& P) {
   return jac_add(t3, jac_neg(P));
 }
 
-// hash_to_G2(msg) -> Jacobian point (caller converts to affine)
-BLS_HDNI g2j hash_to_g2_jac(const uint8_t msg[32]) {
-  fp2 u0, u1;
-  hash_to_field_fp2x2(msg, u0, u1);
-  fp2 Zu2_0 = fp2_mul(SSWU_Z, fp2_sqr(u0));
-  fp2 Zu2_1 = fp2_mul(SSWU_Z, fp2_sqr(u1));
-  fp2 tv0 = fp2_add(fp2_sqr(Zu2_0), Zu2_0);
-  fp2 tv1 = fp2_add(fp2_sqr(Zu2_1), Zu2_1);
-  bool z0 = fp2_is_zero(tv0), z1 = fp2_is_zero(tv1);
-  fp2 a0 = fp2_select(z0, fp2_one(), tv0);
-  fp2 a1 = fp2_select(z1, fp2_one(), tv1);
-  fp2 inv = fp2_inv(fp2_mul(a0, a1));
-  fp2 inv0 = fp2_select(z0, fp2_zero(), fp2_mul(inv, a1));
-  fp2 inv1 = fp2_select(z1, fp2_zero(), fp2_mul(inv, a0));
-  g2a q0 = sswu_map(u0, Zu2_0, tv0, inv0);
-  g2a q1 = sswu_map(u1, Zu2_1, tv1, inv1);
+// hash_to_G2 in two halves around the one inversion of the two maps, so a kernel can batch that inversion over
+// many messages (k_hash.hip + k_inv.hip):
+//   prep:   u0, u1 = hash_to_field(msg); Zu2_j = Z u_j^2; tv_j = Zu2_j^2 + Zu2_j; d = a0 a1 (a_j = tv_j, or 1
+//           when tv_j = 0 -- then inv0(tv_j) = 0, RFC 9380 inv0); d != 0
+//   finish: given d^-1, inv0(tv_j) = d^-1 a_{1-j}, the two SSWU maps, the isogeny, the sum, cofactor clearing.
+struct h2c_prep {
+  fp2 u0, u1, Zu2_0, Zu2_1, tv0, tv1, d;
+};
+BLS_HDNI void hash_to_g2_prep(const uint8_t msg[32], h2c_prep& h) {
+  hash_to_field_fp2x2(msg, h.u0, h.u1);
+  h.Zu2_0 = fp2_mul(SSWU_Z, fp2_sqr(h.u0));
+  h.Zu2_1 = fp2_mul(SSWU_Z, fp2_sqr(h.u1));
+  h.tv0 = fp2_add(fp2_sqr(h.Zu2_0), h.Zu2_0);
+  h.tv1 = fp2_add(fp2_sqr(h.Zu2_1), h.Zu2_1);
+  const fp2 a0 = fp2_select(fp2_is_zero(h.tv0), fp2_one(), h.tv0);
+  const fp2 a1 = fp2_select(fp2_is_zero(h.tv1), fp2_one(), h.tv1);
+  h.d = fp2_mul(a0, a1);
+}
+BLS_HDNI g2j hash_to_g2_finish(const h2c_prep& h, const fp2& dinv) {
+  const bool z0 = fp2_is_zero(h.tv0), z1 = fp2_is_zero(h.tv1);
+  const fp2 a0 = fp2_select(z0, fp2_one(), h.tv0);
+  const fp2 a1 = fp2_select(z1, fp2_one(), h.tv1);
+  const fp2 inv0 = fp2_select(z0, fp2_zero(), fp2_mul(dinv, a1));
+  const fp2 inv1 = fp2_select(z1, fp2_zero(), fp2_mul(dinv, a0));
+  g2a q0 = sswu_map(h.u0, h.Zu2_0, h.tv0, inv0);
+  g2a q1 = sswu_map(h.u1, h.Zu2_1, h.tv1, inv1);
   g2j Q = jac_add(iso3_map_jac(q0), iso3_map_jac(q1));
   return clear_cofactor_g2(Q);
+}
+
+// hash_to_G2(msg) -> Jacobian point (caller converts to affine)
+BLS_HDNI g2j hash_to_g2_jac(const uint8_t msg[32]) {
+  h2c_prep h;
+  hash_to_g2_prep(msg, h);
+  return hash_to_g2_finish(h, fp2_inv(h.d));
 }

@@ -1,8 +1,35 @@
 // A11 hash_to_G2, one lane per DISTINCT signing root of the call (the runtime deduplicates messages: gossip
 // attestations of one committee share AttestationData, reference chain/validation/attestation.ts:131-138).
+// Two kernels around the maps' one field inversion, which is batched over the messages in between
+// (k_inv.hip, Montgomery's simultaneous inversion): k_hash_prep (hash_to_field .. d = a0 a1, stored with
+// N(d)) -> k_batch_inv(N(d)) -> k_hash_map (SSWU x2, isogeny, cofactor clearing; Jacobian H(m) + N(z)) ->
+// k_batch_inv(N(z)) -> k_h_affine.
 #include "k_common.hpp"
 
-STAGE_KERNEL void k_hash_to_g2(PipelineBuffers b) {
+#define W_HPREP (7 * 2 * W_FP)
+
+__device__ __forceinline__ void st_prep(uint32_t* p, uint32_t n, uint32_t u, const h2c_prep& h) {
+  st_fp2(p, n, u, 0 * W_FP, h.u0);
+  st_fp2(p, n, u, 2 * W_FP, h.u1);
+  st_fp2(p, n, u, 4 * W_FP, h.Zu2_0);
+  st_fp2(p, n, u, 6 * W_FP, h.Zu2_1);
+  st_fp2(p, n, u, 8 * W_FP, h.tv0);
+  st_fp2(p, n, u, 10 * W_FP, h.tv1);
+  st_fp2(p, n, u, 12 * W_FP, h.d);
+}
+__device__ __forceinline__ h2c_prep ld_prep(const uint32_t* p, uint32_t n, uint32_t u) {
+  h2c_prep h;
+  h.u0 = ld_fp2(p, n, u, 0 * W_FP);
+  h.u1 = ld_fp2(p, n, u, 2 * W_FP);
+  h.Zu2_0 = ld_fp2(p, n, u, 4 * W_FP);
+  h.Zu2_1 = ld_fp2(p, n, u, 6 * W_FP);
+  h.tv0 = ld_fp2(p, n, u, 8 * W_FP);
+  h.tv1 = ld_fp2(p, n, u, 10 * W_FP);
+  h.d = ld_fp2(p, n, u, 12 * W_FP);
+  return h;
+}
+
+STAGE_KERNEL void k_hash_prep(PipelineBuffers b) {
   uint32_t u = blockIdx.x * WAVE + threadIdx.x;
   if (u >= b.n_umsg) return;
   uint8_t msg[32];
@@ -11,14 +38,29 @@ STAGE_KERNEL void k_hash_to_g2(PipelineBuffers b) {
   uint32_t w[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
 #pragma unroll
   for (int k = 0; k < 32; k++) msg[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-  // Jacobian out; the affine conversion is batched over the messages (k_inv.hip k_h_affine)
-  const g2j h = hash_to_g2_jac(msg);
-  st_g2j(b.h_jac, b.nm, u, h);
-  st_fp(b.h_norm, b.nm, u, 0, fp2_norm(h.z));
+  h2c_prep h;
+  hash_to_g2_prep(msg, h);
+  st_prep(b.h_prep, b.nm, u, h);
+  st_fp(b.h_norm, b.nm, u, 0, fp2_norm(h.d));
+}
+
+// inv: 1 / N(d) from the batch inversion; d^-1 = conj(d) / N(d).  Jacobian out (affine conversion batched).
+STAGE_KERNEL void k_hash_map(PipelineBuffers b, const uint32_t* inv) {
+  uint32_t u = blockIdx.x * WAVE + threadIdx.x;
+  if (u >= b.n_umsg) return;
+  const h2c_prep h = ld_prep(b.h_prep, b.nm, u);
+  const fp ni = ld_fp(inv, b.n_umsg, u, 0);
+  const fp2 dinv = fp2_make(fp_mul(h.d.c0, ni), fp_neg(fp_mul(h.d.c1, ni)));
+  const g2j H = hash_to_g2_finish(h, dinv);
+  st_g2j(b.h_jac, b.nm, u, H);
+  st_fp(b.h_norm, b.nm, u, 0, fp2_norm(H.z));
 }
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
 void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s) {
-  if (b.n_umsg) hipLaunchKernelGGL(k_hash_to_g2, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
+  if (!b.n_umsg) return;
+  hipLaunchKernelGGL(k_hash_prep, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
+  launch_batch_inv(b.h_norm, b.nm, 0, b.inv_buf, b.n_umsg, s);
+  hipLaunchKernelGGL(k_hash_map, grid_for(b.n_umsg), dim3(WAVE), 0, s, b, b.inv_buf);
 }

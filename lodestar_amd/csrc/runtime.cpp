@@ -471,7 +471,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   sl.d_F.ensure((size_t)W_FP12 * max_ranges);
   // work area: per set sig_aff, pk_jac, pk_aff, rsig, f_set (+ per unit unit_p, f_unit), per message h_aff
   const size_t per_set = W_G2A + W_G1J + W_G1A + W_G2J + W_FP12 + 8 * W_G2J + W_FP + (merged ? W_G1A : 0);
-  sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * (W_G2A + W_G2J + W_FP));
+  sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * (W_G2A + W_G2J + W_FP + 14 * W_FP));
   sl.d_lines.ensure((size_t)nm * kMillerLineWords);
   hipStream_t s = sl.stream;
   uint8_t* const din = sl.d_in.p;
@@ -519,7 +519,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.inv_buf = w; w += (size_t)stride * W_FP;  // n_umsg <= n
   pb.h_aff = w; w += (size_t)nm * W_G2A;
   pb.h_jac = w; w += (size_t)nm * W_G2J;
-  pb.h_norm = w;
+  pb.h_norm = w; w += (size_t)nm * W_FP;
+  pb.h_prep = w;
   pb.lines = sl.d_lines.p;
   uint8_t* const db = sl.d_bytes.p;
   pb.flags = db + ob_flags;
