@@ -217,47 +217,65 @@ def stage_mults(n_sets, group_count, pubkeys_per_set, miller_k=2, n_messages=Non
     return mults, oc["products_per_mul"]
 
 
-def roofline(stage_ms_avg, n_sets, group_count, pubkeys_per_set, sets_per_s, miller_k=2, n_messages=None):
-    """Dominant kernel: algorithmic limb products per launch / its average duration (HIP events on its
-    stream, isolated profiled pass) against the measured v_mad_u64_u32 peak.  `pipeline_frac` is the whole
-    chip over the timed (pipelined) region: algorithmic products/s at the measured sets/s over the peak."""
-    mults, ppm = stage_mults(n_sets, group_count, pubkeys_per_set, miller_k, n_messages)
+def roofline(runs, n_sets, group_count, pubkeys_per_set, sets_per_s, miller_k=2, n_messages=None, isolated=None):
+    """Dominant kernel: algorithmic limb products per launch / its average launch duration, against the measured
+    v_mad_u64_u32 peak.  `runs` are the pipeline runs of the TIMED region, each (stage_ms[8], run_sets, groups,
+    distinct messages): HIP events on the stream each stage was launched on, recorded by the runtime while the
+    bench ran (a slot that merged queued calls times the merged run, so one launch covers run_sets sets).
+    Per stage, achieved = sum of its algorithmic products over the runs / sum of its durations.  `pipeline_frac`
+    is the whole chip over the timed region: algorithmic products/s at the measured sets/s over the peak."""
     from lodestar_amd.native import STAGES, KERNEL_OF_STAGE
 
-    best = max(range(len(STAGES)), key=lambda k: stage_ms_avg[k])
-    name = STAGES[best]
-    ms = stage_ms_avg[best]
-    achieved = mults[name] * ppm / (ms * 1e-3) / 1e12
-    per_stage = {STAGES[k]: {"ms": round(stage_ms_avg[k], 4),
-                             "tproducts_per_s": round(mults[STAGES[k]] * ppm / max(stage_ms_avg[k], 1e-9) / 1e9, 3)}
+    prod = np.zeros(len(STAGES))
+    ms = np.zeros(len(STAGES))
+    ppm = 288
+    for st_ms, rs, g, nm in runs:
+        mults, ppm = stage_mults(rs, g, pubkeys_per_set, miller_k, nm)
+        prod += np.array([mults[k] for k in STAGES]) * ppm
+        ms += np.array(st_ms[:len(STAGES)])
+    best = int(np.argmax(ms))
+    achieved = prod[best] / (ms[best] * 1e-3) / 1e12
+    n_runs = max(len(runs), 1)
+    per_stage = {STAGES[k]: {"ms_per_launch": round(ms[k] / n_runs, 4),
+                             "tproducts_per_s": round(prod[k] / max(ms[k] * 1e-3, 1e-12) / 1e12, 3)}
                  for k in range(len(STAGES))}
-    total_products = sum(mults.values()) * ppm
-    pipe = total_products / n_sets * sets_per_s
-    return {
+    mults1, ppm = stage_mults(n_sets, group_count, pubkeys_per_set, miller_k, n_messages)
+    pipe = sum(mults1.values()) * ppm / n_sets * sets_per_s
+    out = {
         "bound": "valu-int",
         "kernel": KERNEL_OF_STAGE[best],
         "achieved": round(achieved, 4),
         "peak": round(VALU_PEAK_PRODUCTS / 1e12, 4),
         "unit": "T limb-products/s (32x32->64)",
         "frac": round(achieved * 1e12 / VALU_PEAK_PRODUCTS, 5),
-        "traffic": pmc_traffic(KERNEL_OF_STAGE[best], n_sets),
-        "algorithmic_products_per_launch": mults[name] * ppm,
-        "pipeline_products_per_step": total_products,
+        "traffic": pmc_traffic(KERNEL_OF_STAGE[best], int(round(np.mean([r[1] for r in runs]))) if runs else 0),
+        "launches_timed": len(runs),
+        "sets_per_launch": round(float(np.mean([r[1] for r in runs])), 1) if runs else 0,
+        "algorithmic_products_per_launch": round(prod[best] / n_runs),
+        "avg_launch_ms": round(ms[best] / n_runs, 4),
+        "pipeline_products_per_set": round(sum(mults1.values()) * ppm / n_sets),
         "pipeline_achieved": round(pipe / 1e12, 4),
         "pipeline_frac": round(pipe / VALU_PEAK_PRODUCTS, 5),
         "stages": per_stage,
     }
+    if isolated is not None:
+        mi, _ = stage_mults(n_sets, group_count, pubkeys_per_set, miller_k, n_messages)
+        out["isolated_call"] = {STAGES[k]: {"ms": round(isolated[k], 4),
+                                            "tproducts_per_s": round(mi[STAGES[k]] * ppm / max(isolated[k], 1e-9) / 1e9, 3)}
+                                for k in range(len(STAGES))}
+    return out
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-PMC_SETS_PER_LAUNCH = 16384  # the C2 launch the counters were collected on (tools/gpurun/pmc.sh)
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+PMC_SETS_PER_LAUNCH = 16384  # the C2 launch the counters were collected on (tools/gpurun/r02_pmc.sh)
 
 
 def pmc_traffic(kernel, n_sets):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (FETCH_SIZE doubled for the
-    gfx950 half-count of wide reads, WRITE_SIZE as is; MI355X_MICROARCH.md HBM section), or None when the
-    counters were collected on a different launch size."""
-    if n_sets != PMC_SETS_PER_LAUNCH or not os.path.exists(PMC_FILE):
+    gfx950 half-count of wide reads, WRITE_SIZE as is; MI355X_MICROARCH.md HBM section), collected on
+    16,384-set launches and scaled linearly to an n_sets launch (every stage is lane-per-set, so its traffic --
+    inputs, outputs, scratch -- is per set); None when no PMC file is committed."""
+    if not n_sets or not os.path.exists(PMC_FILE):
         return None
     with open(PMC_FILE) as fh:
         table = json.load(fh)["kernels"]
@@ -265,8 +283,9 @@ def pmc_traffic(kernel, n_sets):
     parts = {"k_miller_sets": ["k_miller_lines", "k_miller_acc"]}.get(kernel, [kernel])
     if not all(p in table for p in parts):
         return None
-    return round(sum(2 * 1024 * table[p]["FETCH_SIZE_kB_per_launch"] + 1024 * table[p]["WRITE_SIZE_kB_per_launch"]
-                     for p in parts))
+    b16k = sum(2 * 1024 * table[p]["FETCH_SIZE_kB_per_launch"] + 1024 * table[p]["WRITE_SIZE_kB_per_launch"]
+               for p in parts)
+    return round(b16k * n_sets / PMC_SETS_PER_LAUNCH)
 
 
 BLST_SETS_PER_CORE = 2200.0  # published anchor: ~0.9 ms/set/thread, x2 batched
@@ -310,16 +329,22 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--group-sets", type=int, default=256)
-    ap.add_argument("--inflight", type=int, default=12,
+    ap.add_argument("--inflight", type=int, default=32,
                     help="verifySignatureSets calls in flight per GPU (runtime slots); 1 = strictly serial")
+    ap.add_argument("--slots", type=int, default=4,
+                    help="runtime slots per GPU (0 = one per in-flight call); fewer slots than calls in flight make "
+                         "each slot merge the queued calls into one pipeline run")
+    ap.add_argument("--merge-sets", type=int, default=131072, help="max sets of one merged pipeline run (0 = never)")
     ap.add_argument("--miller-k", type=int, default=2, help="pairings per Miller accumulator (shared squarings)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
 
     # Concurrent calls use one runtime slot (HIP stream) each; HIP reads GPU_MAX_HW_QUEUES once, at its first
-    # call, so the launcher sets it (the box default of 4 makes 12 slot streams share 4 in-order queues).
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    # call, so the launcher sets it.  The box exports 4, which makes the slot streams share 4 in-order queues:
+    # 1.57M vs 2.23M sets/s with 8 (profiles/r02_hwq_env.json), so a smaller inherited value is raised.
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -342,7 +367,8 @@ def main():
     devices = list(range(n_dev)) if world == 1 else [local_rank]
     ctx = Context(devices)
     ctx.set_option("group_sets", args.group_sets)
-    ctx.set_option("slots", max(1, args.inflight))
+    ctx.set_option("slots", max(1, args.slots or args.inflight))
+    ctx.set_option("merge_sets", args.merge_sets)
     ctx.set_option("miller_k", args.miller_k)
     work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev)
     call = dict(work)
@@ -352,12 +378,14 @@ def main():
         expected = np.ones(len(call["job_first_set"]) - 1, np.int8)
 
     def step(_=None):
+        t1 = time.perf_counter()
         res, st = ctx.verify_raw(**call, seed=SEED)
+        lat_ms = (time.perf_counter() - t1) * 1e3
         if not np.array_equal(res, expected):
             bad = np.nonzero(res != expected)[0]
             raise SystemExit(f"verification mismatch on {len(bad)} jobs (first {bad[:8]}: got {res[bad[:8]]}, "
                              f"want {expected[bad[:8]]})")
-        return st
+        return st, lat_ms
 
     pool = ThreadPoolExecutor(max_workers=max(1, args.inflight))  # ctypes releases the GIL inside the call
     for _ in range(args.warmup):
@@ -373,15 +401,20 @@ def main():
         sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
     except Exception:  # torch is plumbing only; every step is complete when its call returns
         sync = lambda: None
+    # per-stage HIP events on each slot's stream, recorded by the runtime during the timed region (roofline)
+    if not args.no_profile:
+        ctx.set_option("profile", 1)
     # ---- timed region: K steps, up to `inflight` of them on the GPU at once ----
     barrier()
     sync()
     t0 = time.perf_counter()
-    stats = list(pool.map(step, range(args.steps)))
+    results = list(pool.map(step, range(args.steps)))
     sync()
     barrier()
     dt = time.perf_counter() - t0
-    groups = stats[-1].groups
+    ctx.set_option("profile", 0)
+    stats = [r[0] for r in results]
+    call_lat = np.array([r[1] for r in results])
     from lodestar_amd.shard import max_over_ranks
 
     dt = max_over_ranks(dt, dist)
@@ -389,12 +422,12 @@ def main():
     total_sets = (desc["total_sets_per_step"] if strong else n_sets * world) * args.steps
     n_gpus = world * n_dev
     value = total_sets / dt
-    # ---- isolated batches (untimed): p50 latency of one call, and per-stage kernel times ----
+    # ---- isolated batches (untimed): p50 latency of one call alone, and its per-stage kernel times ----
     lat = []
     for _ in range(3):
-        t1 = time.perf_counter()
-        step()
-        lat.append((time.perf_counter() - t1) * 1e3)
+        st_iso, l_ms = step()
+        lat.append(l_ms)
+    groups, n_msgs = st_iso.groups, st_iso.unique_messages  # one call alone: its own groups / distinct messages
     out = {
         "metric": "verified signature sets/sec (node)",
         "miller_k": args.miller_k,
@@ -410,17 +443,22 @@ def main():
         "dtype": "u32/u64 (28-bit-limb Montgomery integer arithmetic)",
         "data": "synthetic (interop keys, SHA-256 messages, signatures generated on the GPU before timing)",
         "config": dict(desc, group_sets=args.group_sets, batch_groups_per_step=groups, inflight=args.inflight,
+                       slots=args.slots or args.inflight, merge_sets=args.merge_sets,
                        parallelism=f"shard-by-job x{n_gpus} ({'one process per GPU' if world > 1 else 'in-process devices'}), no collective"),
         "p50_batch_latency_ms": round(float(np.median(lat)), 3),
+        "call_latency_under_load_ms": {"p50": round(float(np.percentile(call_lat, 50)), 2),
+                                       "p99": round(float(np.percentile(call_lat, 99)), 2)},
     }
     if not args.no_profile:
+        runs = [(list(st.stage_ms[:8]), st.run_sets, st.groups, st.unique_messages // n_dev) for st in stats
+                if st.run_sets > 0 and n_dev == 1]
         ctx.set_option("profile", 1)
         stage_acc = np.zeros(8)
         for _ in range(2):
-            stage_acc += np.array(step().stage_ms[:8])
+            stage_acc += np.array(step()[0].stage_ms[:8])
         ctx.set_option("profile", 0)
-        out["roofline"] = roofline(stage_acc / 2, n_sets // n_dev, groups // n_dev, pk_per_set, value / n_gpus,
-                                   args.miller_k, stats[-1].unique_messages // n_dev)
+        out["roofline"] = roofline(runs, n_sets // n_dev, groups // n_dev, pk_per_set, value / n_gpus,
+                                   args.miller_k, n_msgs // n_dev, isolated=stage_acc / 2)
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(dict(call, pks_table=work["pks_table"]) if "pks_table" in work else call,
                                            expected)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define BLSGPU_ABI_VERSION 2
+#define BLSGPU_ABI_VERSION 3
 
 enum blsgpu_code {
   BLSGPU_OK = 0,
@@ -102,6 +102,8 @@ typedef struct blsgpu_stats {
   uint32_t unique_messages; /* distinct signing roots hashed to G2 */
   uint32_t pairing_units;   /* Miller loops of the batch pass (sets, or same-message units) */
   uint32_t miller_chunks;   /* Miller accumulators of the batch pass (miller_k pairings share squarings) */
+  uint32_t run_sets;        /* sets of the pipeline run that stage_ms timed: a runtime slot that merged queued
+                               calls into one run reports it (and stage_ms) on the first call, 0 on the others */
 } blsgpu_stats;
 
 /* Create a context on the given HIP devices (NULL / n <= 0: every visible device).  Each device gets 4

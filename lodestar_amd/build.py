@@ -18,12 +18,27 @@ SOURCES = ["k_sig.hip", "k_hash.hip", "k_pk.hip", "k_miller.hip", "k_group.hip",
            "runtime.cpp"]
 
 
-def _deps():
+OBJ_DIR = os.path.join(PKG, "build")  # per-TU objects, kept so an edit rebuilds only the TUs it touches
+
+
+def _headers():
     out = [os.path.join(ROOT, "include", "blsgpu.h")]
     for f in os.listdir(CSRC):
-        if f.endswith((".hpp", ".h", ".hip", ".cpp")):
+        if f.endswith((".hpp", ".h")):
             out.append(os.path.join(CSRC, f))
     return out
+
+
+def _tu_deps(src):
+    """runtime.cpp sees only the C-ABI header and the kernel launch declarations; a kernel TU sees every
+    arithmetic header."""
+    if src.endswith(".cpp"):
+        return [os.path.join(CSRC, src), os.path.join(CSRC, "kernels.h"), os.path.join(ROOT, "include", "blsgpu.h")]
+    return [os.path.join(CSRC, src)] + _headers()
+
+
+def _deps():
+    return _headers() + [os.path.join(CSRC, s) for s in SOURCES]
 
 
 def up_to_date():
@@ -39,13 +54,19 @@ def build(force=False, verbose=True):
         return LIB
     objs = []
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include")]
-    common += ["-D" + d for d in os.environ.get("BLSGPU_DEFINES", "").split()]  # e.g. BLSGPU_WPE=2
+    defines = os.environ.get("BLSGPU_DEFINES", "").split()  # e.g. BLSGPU_WPE=2
+    common += ["-D" + d for d in defines]
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    # objects are keyed by the library name and the defines, so variant builds never reuse each other's objects
+    key = os.path.splitext(os.path.basename(LIB))[0] + ("." + "_".join(defines).replace("=", "-") if defines else "")
     # one translation unit per pipeline stage, compiled in parallel (the stage kernels are large)
     procs = []
     t0 = time.time()
     for src in SOURCES:
-        obj = os.path.splitext(LIB)[0] + "." + os.path.splitext(src)[0] + ".o"
+        obj = os.path.join(OBJ_DIR, key + "." + os.path.splitext(src)[0] + ".o")
         objs.append(obj)
+        if not force and os.path.exists(obj) and all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in _tu_deps(src)):
+            continue
         cmd = [HIPCC] + common + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
@@ -59,8 +80,6 @@ def build(force=False, verbose=True):
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    for o in objs:
-        os.remove(o)
     build_node_addon(verbose=verbose)
     return LIB
 

@@ -566,6 +566,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   st.unique_messages += n_umsg;
   st.pairing_units += merged ? n_units : n;
   st.miller_chunks += n_chunks;
+  st.run_sets = n;
   if (prof) {
     for (int k = 0; k < kStages; k++) {
       float ms = 0;
@@ -695,6 +696,7 @@ void finish_call(Call* c) {
     local.miller_chunks += c->sst[k].miller_chunks;
     if (c->rc[k] != BLSGPU_OK && c->rc[k] != BLSGPU_DEVICE_ERROR) status = c->rc[k];
   }
+  local.run_sets = c->sst.empty() ? 0 : c->sst[0].run_sets;
   local.devices_used = (uint32_t)c->shards.size();
   local.device_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->t0).count();
   if (c->stats) *c->stats = local;

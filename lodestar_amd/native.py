@@ -70,6 +70,7 @@ class Stats(ctypes.Structure):
         ("unique_messages", ctypes.c_uint32),
         ("pairing_units", ctypes.c_uint32),
         ("miller_chunks", ctypes.c_uint32),
+        ("run_sets", ctypes.c_uint32),
     ]
 
 
