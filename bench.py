@@ -209,9 +209,9 @@ def stage_mults(n_sets, group_count, pubkeys_per_set, miller_k=2, n_messages=Non
         "hash_to_g2": per_set["hash_to_g2"] * (n_messages or n_sets),
         "pk_aggregate": oc["pk_aggregate_per_pubkey"] * n_sets * pubkeys_per_set if pubkeys_per_set > 1 else 0.0,
         "pk_finish": per_set["pk_finish"] * n_sets,
-        "sig_scale": per_set["sig_scale"] * n_sets,
+        "sig_msm": per_set["sig_msm"] * n_sets + pgf["sig_msm"] * group_count,
         "miller_sets": per_set["miller_sets"] * n_sets,
-        "group_reduce": (pgs["group_sig_miller"] + pgs["group_finish"]) * n_sets,
+        "group_reduce": pgs["group_finish"] * n_sets,
         "group_check": (pgf["group_sig_miller"] + pgf["group_finish"]) * group_count,
     }
     return mults, oc["products_per_mul"]

@@ -96,7 +96,7 @@ typedef struct blsgpu_stats {
   uint32_t devices_used;
   double device_ms; /* wall time of the call from dispatch to completion */
   /* With option "profile" = 1: per-stage kernel time (HIP events on the launch stream, device 0 shard):
-   * 0 sig_decode 1 hash_to_g2 2 pk_aggregate 3 pk_finish 4 sig_scale 5 miller_sets
+   * 0 sig_decode 1 hash_to_g2 2 pk_aggregate 3 pk_finish 4 sig_msm 5 miller_sets
    * 6 group_sig_miller 7 group_finish */
   double stage_ms[8];
   uint32_t unique_messages; /* distinct signing roots hashed to G2 */

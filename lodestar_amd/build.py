@@ -14,7 +14,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.environ.get("BLSGPU_LIB") or os.path.join(PKG, "libblsgpu.so")  # override: tuning variants
 ARCH = os.environ.get("BLSGPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["k_sig.hip", "k_hash.hip", "k_pk.hip", "k_miller.hip", "k_group.hip", "k_inv.hip", "k_ssz.hip", "k_debug.hip",
+SOURCES = ["k_sig.hip", "k_msm.hip", "k_hash.hip", "k_pk.hip", "k_miller.hip", "k_group.hip", "k_inv.hip", "k_ssz.hip", "k_debug.hip",
            "runtime.cpp"]
 
 

@@ -3,8 +3,8 @@
 // A batch group is a contiguous range of clean jobs checked with ONE final exponentiation:
 //   prod_i e(r_i pk_i, H(m_i)) * e(-g1, sum_i r_i sig_i) == 1
 // The Miller values (chunks of sets or same-message units) were computed by k_miller_acc; here
-//   k_group_reduce   one wave per group: S = sum r_i sig_i (G2) and F = prod f (Fp12), each lane a strided
-//                    partial, then a 6-level LDS tree (64 -> 1)
+//   k_group_reduce   one wave per group: F = prod f (Fp12), each lane a strided partial, then a 6-level LDS
+//                    tree (64 -> 1); S = sum r_i sig_i comes from the bucket MSM (k_msm.hip)
 //   k_group_check    one 128-lane workgroup per group: FinalExp(F * MillerLoop(-g1, S)) == 1, as
 //                    workgroup-cooperative Fp12 arithmetic (gt_wave.hpp)
 // The same two kernels re-check the sub-ranges of a failed group when the host bisects it
@@ -33,8 +33,8 @@ __global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const 
   __shared__ uint32_t red[WAVE * W_FP12];
   const uint32_t g = blockIdx.x, lane = threadIdx.x;
   if (g >= ng) return;
-  // ---- S = sum r_i sig_i over the group's included sets
-  {
+  // ---- S = sum r_i sig_i over the group's included sets (only without the MSM stage)
+  if (set_ranges) {
     const uint32_t first = set_ranges[2 * g], last = set_ranges[2 * g + 1];
     g2j S = jac_infinity<fp2>();
     for (uint32_t i = first + lane; i < last; i += WAVE)

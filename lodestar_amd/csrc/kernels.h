@@ -89,6 +89,14 @@ void launch_batch_inv(const uint32_t* src, uint32_t src_stride, int w0, uint32_t
 void launch_pk_affine(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 void launch_h_affine(const PipelineBuffers& b, hipStream_t s);
 void launch_sig_scale(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
+// S_r = sum r_i sig_i over the included sets of each range, as a bucket MSM (k_msm.hip, msm.hpp).  Range r is the
+// slices [range_slices[r], range_slices[r+1]); slice s is the sets [slices[2s], slices[2s+1]) (<= MSM_SLICE of
+// them).  B: MSM_BUCKET_WORDS words per slice, W: MSM_WINDOW_WORDS per range; S: W_G2J SoA, stride n_ranges.
+#define MSM_SLICE 256
+#define MSM_BUCKET_WORDS (128 * W_G2J)
+#define MSM_WINDOW_WORDS (16 * W_G2J)
+void launch_sig_msm(const PipelineBuffers& b, const uint32_t* slices, uint32_t n_slices, const uint32_t* range_slices,
+                    uint32_t n_ranges, uint32_t* B, uint32_t* W, uint32_t* S, hipStream_t s);
 // per-job error status and the per-set include mask of the batch equation
 void launch_job_mask(const PipelineBuffers& b, hipStream_t s);
 // P_u = sum over the unit's included sets of r_i pk_i (affine)
@@ -100,7 +108,8 @@ void launch_miller_lines(const PipelineBuffers& b, hipStream_t s);
 void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s);
 // Batch groups: group g covers sets [set_ranges[2g], set_ranges[2g+1]) (S over included sets) and Miller
 // chunks [f_ranges[2g], f_ranges[2g+1]).
-// reduce: S_g = sum r_i sig_i (W_G2J SoA, stride n_groups), F_g = prod f_chunk (W_FP12 SoA, stride n_groups)
+// reduce: F_g = prod f_chunk (W_FP12 SoA, stride n_groups), and, when set_ranges is not null, S_g = sum r_i rsig_i
+// (W_G2J SoA, stride n_groups) from per-set scalings (the pipeline computes S with launch_sig_msm instead)
 void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
                          uint32_t n_groups, uint32_t* S, uint32_t* F, hipStream_t s);
 // check: ok_g = FinalExp(F_g * MillerLoop(-g1, S_g)) == 1

@@ -99,13 +99,14 @@ struct Slot {
   // d_in / h_in: every per-call input packed into one arena (one H2D transfer); d_res / h_res: job errors +
   // group verdicts (one D2H transfer).
   DevBuf<uint8_t> d_in, d_res, d_bytes, d_ok;
-  DevBuf<uint32_t> d_work, d_lines, d_S, d_F, d_list;
+  DevBuf<uint32_t> d_work, d_lines, d_S, d_F, d_list, d_msmB, d_msmW;
   HostBuf<uint8_t> h_in, h_res, h_ok;
   HostBuf<uint32_t> h_list;
 
   void release_all() {
     d_in.release(); d_res.release(); d_bytes.release(); d_ok.release();
     d_work.release(); d_lines.release(); d_S.release(); d_F.release(); d_list.release();
+    d_msmB.release(); d_msmW.release();
     h_in.release(); h_res.release(); h_ok.release(); h_list.release();
   }
 };
@@ -164,6 +165,16 @@ inline std::pair<uint32_t, uint32_t> add_chunks(std::vector<uint32_t>& first, st
     first.push_back((uint32_t)items.size());
   }
   return {c0, (uint32_t)first.size() - 1};
+}
+
+// Splits set ranges into MSM slices of <= MSM_SLICE sets: appends to slices (pairs), returns the range's
+// [first slice, end slice)
+inline void add_slices(std::vector<uint32_t>& slices, std::vector<uint32_t>& range_slices, uint32_t a, uint32_t e) {
+  for (uint32_t x = a; x < e; x += MSM_SLICE) {
+    slices.push_back(x);
+    slices.push_back(std::min<uint32_t>(e, x + MSM_SLICE));
+  }
+  range_slices.push_back((uint32_t)(slices.size() / 2));
 }
 
 struct Shard {
@@ -390,6 +401,11 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     g_chunks[2 * g + 1] = cr.second;
   }
   const uint32_t n_chunks = (uint32_t)chunk_first.size() - 1;
+  // MSM slices of the groups' set ranges (S_g = sum r_i sig_i)
+  std::vector<uint32_t> slices, range_slices{0};
+  for (uint32_t g = 0; g < ng0; g++)
+    add_slices(slices, range_slices, job_sets(group_jobs[g].first).first, job_sets(group_jobs[g].second - 1).second);
+  const uint32_t n_slices = (uint32_t)(slices.size() / 2);
   // sets that aggregate >= 2 keys (one wave each in k_pk_aggregate); one-key sets are read by k_pk_finish
   std::vector<uint32_t> agg_sets;
   if (table_mode || bytes_agg)
@@ -406,7 +422,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
                o_ufirst = al256(o_franges + (size_t)std::max(ng0, 1u) * 8),
                o_usets = al256(o_ufirst + (size_t)(n_units + 1) * 4), o_umsgi = al256(o_usets + (size_t)unit_sets.size() * 4),
                o_cfirst = al256(o_umsgi + (size_t)n_units * 4), o_citems = al256(o_cfirst + (size_t)(n_chunks + 1) * 4),
-               o_agg = al256(o_citems + chunk_items.size() * 4), o_pk = al256(o_agg + agg_sets.size() * 4);
+               o_agg = al256(o_citems + chunk_items.size() * 4), o_slices = al256(o_agg + agg_sets.size() * 4),
+               o_rslices = al256(o_slices + slices.size() * 4), o_pk = al256(o_rslices + range_slices.size() * 4);
   size_t in_bytes;
   if (table_mode)
     in_bytes = al256(o_pk + (size_t)(n + 1) * 4) + (size_t)npk * 4;
@@ -443,6 +460,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   memcpy(hin + o_cfirst, chunk_first.data(), chunk_first.size() * 4);
   memcpy(hin + o_citems, chunk_items.data(), chunk_items.size() * 4);
   if (!agg_sets.empty()) memcpy(hin + o_agg, agg_sets.data(), agg_sets.size() * 4);
+  if (!slices.empty()) memcpy(hin + o_slices, slices.data(), slices.size() * 4);
+  memcpy(hin + o_rslices, range_slices.data(), range_slices.size() * 4);
   if (merged) {
     memcpy(hin + o_ufirst, unit_first.data(), (size_t)(n_units + 1) * 4);
     memcpy(hin + o_usets, unit_sets.data(), unit_sets.size() * 4);
@@ -469,8 +488,11 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   sl.h_res.ensure(res_bytes);
   sl.d_S.ensure((size_t)W_G2J * max_ranges);
   sl.d_F.ensure((size_t)W_FP12 * max_ranges);
-  // work area: per set sig_aff, pk_jac, pk_aff, rsig, f_set (+ per unit unit_p, f_unit), per message h_aff
-  const size_t per_set = W_G2A + W_G1J + W_G1A + W_G2J + W_FP12 + 8 * W_G2J + W_FP + (merged ? W_G1A : 0);
+  sl.d_msmB.ensure((size_t)MSM_BUCKET_WORDS * std::max<uint32_t>(n_slices, 1));
+  sl.d_msmW.ensure((size_t)MSM_WINDOW_WORDS * max_ranges);
+  // work area: per set sig_aff, pk_jac, pk_aff, f_chunk, the G1 window table of r_i pk_i, inv_buf (+ per unit
+  // unit_p), per message h_aff, h_jac, h_norm, h_prep
+  const size_t per_set = W_G2A + W_G1J + W_G1A + W_FP12 + 8 * W_G1J + W_FP + (merged ? W_G1A : 0);
   sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * (W_G2A + W_G2J + W_FP + 14 * W_FP));
   sl.d_lines.ensure((size_t)nm * kMillerLineWords);
   hipStream_t s = sl.stream;
@@ -507,9 +529,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.sig_aff = w; w += (size_t)stride * W_G2A;
   pb.pk_jac = w; w += (size_t)stride * W_G1J;
   pb.pk_aff = w; w += (size_t)stride * W_G1A;
-  pb.rsig = w; w += (size_t)stride * W_G2J;
+  pb.rsig = nullptr;  // S comes from the MSM (k_msm.hip), not from per-set scalings
   pb.f_chunk = w; w += (size_t)stride * W_FP12;
-  pb.scal_tab = w; w += (size_t)stride * 8 * W_G2J;
+  pb.scal_tab = w; w += (size_t)stride * 8 * W_G1J;
   if (merged) {
     pb.unit_p = w; w += (size_t)stride * W_G1A;
   }
@@ -546,8 +568,10 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   launch_pk_finish(pb, n, s);
   launch_pk_affine(pb, n, s);
   mark(4);
-  launch_sig_scale(pb, n, s);
   launch_job_mask(pb, s);
+  const uint32_t* d_slices = reinterpret_cast<uint32_t*>(din + o_slices);
+  const uint32_t* d_rslices = reinterpret_cast<uint32_t*>(din + o_rslices);
+  launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s);
   mark(5);
   launch_miller_lines(pb, s);
   if (merged) launch_unit_aggregate(pb, s);
@@ -555,7 +579,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   mark(6);
   const uint32_t* d_ranges = reinterpret_cast<uint32_t*>(din + o_ranges);
   const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
-  launch_group_reduce(pb, d_ranges, d_franges, ng0, sl.d_S.p, sl.d_F.p, s);
+  (void)d_ranges;
+  launch_group_reduce(pb, nullptr, d_franges, ng0, sl.d_S.p, sl.d_F.p, s);
   mark(7);
   launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, s);
   mark(8);
@@ -603,17 +628,20 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // Each retried job gets its own set range (S) and its own Miller chunks (its sets, miller_k per chunk).
   if (!retry.empty()) {
     const uint32_t nr = (uint32_t)retry.size();
-    std::vector<uint32_t> rfirst{0}, ritems, rr(2 * (size_t)nr), rf(2 * (size_t)nr);
+    std::vector<uint32_t> rfirst{0}, ritems, rr(2 * (size_t)nr), rf(2 * (size_t)nr), rsl, rrs{0};
     for (uint32_t q = 0; q < nr; q++) {
       const auto js = job_sets(retry[q]);
       rr[2 * q] = js.first;
       rr[2 * q + 1] = js.second;
+      add_slices(rsl, rrs, js.first, js.second);
       const auto cr = add_chunks(rfirst, ritems, js.first, js.second, mk);
       rf[2 * q] = cr.first;
       rf[2 * q + 1] = cr.second;
     }
     const uint32_t nc = (uint32_t)rfirst.size() - 1;
-    const size_t words = 4 * (size_t)nr + rfirst.size() + ritems.size();
+    const uint32_t nrs = (uint32_t)(rsl.size() / 2);
+    const size_t o_rsl = 4 * (size_t)nr + rfirst.size() + ritems.size(), o_rrs = o_rsl + rsl.size();
+    const size_t words = o_rrs + rrs.size();
     sl.h_list.ensure(words);
     sl.d_list.ensure(words);
     uint32_t* hl = sl.h_list.p;
@@ -621,6 +649,10 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     memcpy(hl + 2 * (size_t)nr, rf.data(), rf.size() * 4);
     memcpy(hl + 4 * (size_t)nr, rfirst.data(), rfirst.size() * 4);
     memcpy(hl + 4 * (size_t)nr + rfirst.size(), ritems.data(), ritems.size() * 4);
+    memcpy(hl + o_rsl, rsl.data(), rsl.size() * 4);
+    memcpy(hl + o_rrs, rrs.data(), rrs.size() * 4);
+    sl.d_msmB.ensure((size_t)MSM_BUCKET_WORDS * std::max<uint32_t>(nrs, 1));
+    sl.d_msmW.ensure((size_t)MSM_WINDOW_WORDS * nr);
     sl.d_ok.ensure(nr);
     sl.h_ok.ensure(nr);
     sl.d_S.ensure((size_t)W_G2J * nr);
@@ -631,7 +663,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     pr.chunk_first = sl.d_list.p + 4 * (size_t)nr;
     pr.chunk_items = sl.d_list.p + 4 * (size_t)nr + rfirst.size();
     launch_miller_acc(pr, false, s);
-    launch_group_reduce(pr, sl.d_list.p, sl.d_list.p + 2 * (size_t)nr, nr, sl.d_S.p, sl.d_F.p, s);
+    launch_sig_msm(pr, sl.d_list.p + o_rsl, nrs, sl.d_list.p + o_rrs, nr, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s);
+    launch_group_reduce(pr, nullptr, sl.d_list.p + 2 * (size_t)nr, nr, sl.d_S.p, sl.d_F.p, s);
     launch_group_check(sl.d_S.p, sl.d_F.p, nr, sl.d_ok.p, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, nr, hipMemcpyDeviceToHost, s));

@@ -74,9 +74,9 @@ class Stats(ctypes.Structure):
     ]
 
 
-STAGES = ["sig_decode", "hash_to_g2", "pk_aggregate", "pk_finish", "sig_scale", "miller_sets",
+STAGES = ["sig_decode", "hash_to_g2", "pk_aggregate", "pk_finish", "sig_msm", "miller_sets",
           "group_reduce", "group_check"]
-KERNEL_OF_STAGE = ["k_sig_decode", "k_hash_map", "k_pk_aggregate", "k_pk_finish", "k_sig_scale",
+KERNEL_OF_STAGE = ["k_sig_decode", "k_hash_map", "k_pk_aggregate", "k_pk_finish", "k_msm_bucket",
                    "k_miller_sets", "k_group_reduce", "k_group_check"]
 
 

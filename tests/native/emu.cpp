@@ -3,6 +3,7 @@
 // into libblsgpu.so (the product has no CPU path).  Byte formats: canonical big-endian 48-byte Fp.
 #include <string.h>
 #include "../../lodestar_amd/csrc/ops.hpp"
+#include "../../lodestar_amd/csrc/msm.hpp"
 
 #if defined(BLS_COUNT_OPS)
 unsigned long long bls_count_mul = 0, bls_count_sqr = 0;
@@ -72,8 +73,51 @@ static jac<F> emu_mul_scalar_word(const jac<F>& P, uint64_t w) {
   for (int k = 14; k >= 0; k--) r = jac_add(jac_dbl(jac_dbl(jac_dbl(jac_dbl(r)))), pick(k));
   return r;
 }
+// The bucket MSM of k_msm.hip (msm.hpp) over n affine points with scalar words w: buckets filled in set order
+// (the kernel's list order), then the window sums and the Horner pass.  `active[i] == 0` skips point i.
+static g2j emu_msm_core(const g2a* P, const uint64_t* w, const uint8_t* active, int n) {
+  static g2j B[MSM_WINDOWS][MSM_BUCKETS];
+  for (int k = 0; k < MSM_WINDOWS; k++)
+    for (int e = 0; e < MSM_BUCKETS; e++) B[k][e] = jac_infinity<fp2>();
+  for (int i = 0; i < n; i++) {
+    if (active && !active[i]) continue;
+    for (int k = 0; k < MSM_WINDOWS; k++) {
+      bool neg;
+      const uint32_t e = msm_bucket(w[i], k, neg);
+      g2a q = P[i];
+      if (neg) q.y = fp2_neg(q.y);
+      B[k][e] = jac_add_aff(B[k][e], q);
+    }
+  }
+  static g2j W[MSM_WINDOWS];
+  for (int k = 0; k < MSM_WINDOWS; k++) W[k] = msm_window_sum([&](int e) { return B[k][e]; });
+  return msm_horner([&](int k) { return W[k]; });
+}
 extern "C" {
+// sum_i r_i P_i through the bucket MSM; returns 0 for the point at infinity
+int emu_msm(const uint8_t* pts192, const uint64_t* w, const uint8_t* active, int n, uint8_t* out192) {
+  static g2a P[4096];
+  if (n > 4096) return -1;
+  for (int i = 0; i < n; i++) P[i] = load_g2(pts192 + 192 * (size_t)i);
+  g2a a;
+  if (!jac_to_aff(emu_msm_core(P, w, active, n), a)) return 0;
+  g2a_to_be192(a, out192);
+  return 1;
+}
 #if defined(BLS_COUNT_OPS)
+// bucket MSM over n distinct points (the count covers the MSM only, not the point loads)
+void emu_stage_sig_msm(const uint8_t* pts192, int n) {
+  static g2a P[4096];
+  static uint64_t w[4096];
+  uint64_t z = 0x1234567887654321ull;
+  for (int i = 0; i < n; i++) {
+    P[i] = load_g2(pts192 + 192 * (size_t)i);
+    z = z * 6364136223846793005ull + 1442695040888963407ull;
+    w[i] = z;
+  }
+  bls_count_mul = bls_count_sqr = 0;
+  (void)emu_msm_core(P, w, nullptr, n);
+}
 void emu_count_reset() { bls_count_mul = bls_count_sqr = 0; }
 unsigned long long emu_count_mul() { return bls_count_mul; }
 unsigned long long emu_count_sqr() { return bls_count_sqr; }

@@ -199,3 +199,42 @@ def test_key_validate_matches_c_oracle():
             assert L.emu_key_validate(out.raw, 96, out) == 0
     assert {0, bls.BLST_BAD_ENCODING, bls.BLST_POINT_NOT_ON_CURVE, bls.BLST_POINT_NOT_IN_GROUP,
             bls.BLST_PK_IS_INFINITY} <= seen
+
+
+def _r_of_word(w):
+    """Batch scalar of a 64-bit word (runtime.cpp / k_common.hpp): r = 2w + 1 - 2^64, word 0 = r = 1."""
+    return 1 if w == 0 else 2 * w + 1 - 2**64
+
+
+def test_bucket_msm_matches_sum_of_scalings():
+    """msm.hpp (the k_msm.hip algorithm) against the oracle's sum of r_i P_i: random points and words, r = 1
+    words, skipped points, and the exceptional bucket additions (the same point twice, P and -P)."""
+    L = lib()
+    L.emu_msm.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p, ctypes.c_int,
+                          ctypes.c_char_p]
+    r2 = random.Random(77)
+    base = [bls.g2_mul(bls.G2_GEN, r2.randrange(1, bls.R)) for _ in range(6)]
+    cases = [
+        (base[:1], [r2.getrandbits(64)], None),
+        (base[:1], [0], None),                                   # CoreVerify: r = 1
+        (base[:5], [r2.getrandbits(64) for _ in range(5)], None),
+        (base[:3] + base[:3], [7, 7, 7, 7, 7, 7], None),         # equal points, equal words: bucket doublings
+        (base[:2] + [bls.g2_neg(base[0])], [9, 5, 9], None),     # P and -P with one word: bucket cancellation
+        (base, [r2.getrandbits(64) for _ in range(6)], bytes([1, 0, 1, 1, 0, 1])),
+        (base[:2], [1, 2], bytes([0, 0])),                       # nothing active: infinity
+    ]
+    out = buf(192)
+    for pts, words, active in cases:
+        n = len(pts)
+        W = (ctypes.c_uint64 * n)(*words)
+        got = L.emu_msm(b"".join(g2b(p) for p in pts), W, active, n, out)
+        want = None
+        for i, p in enumerate(pts):
+            if active is not None and not active[i]:
+                continue
+            q = bls.g2_mul(p, _r_of_word(words[i]) % bls.R)
+            want = q if want is None else bls.g2_add(want, q)
+        if want is None:
+            assert got == 0
+        else:
+            assert got == 1 and b2g2(out.raw) == want, (words, active)

@@ -45,18 +45,23 @@ FIELDS = {".vgpr_count": "vgpr", ".agpr_count": "agpr", ".sgpr_count": "sgpr",
 
 
 def parse(notes):
+    # amdhsa.kernels is a YAML list of maps with alphabetically ordered keys: a kernel's record starts at its
+    # list item ("  - .agpr_count: ..."), and .agpr_count / .group_segment_fixed_size come BEFORE its .name
     out, cur = [], None
     for line in notes.splitlines():
+        if re.match(r"^  - \.", line):
+            cur = {}
+            out.append(cur)
         s = line.strip().lstrip("- ").strip()
         m = re.match(r"(\.[a-z_]+):\s+(.*)$", s)
-        if not m:
+        if not m or cur is None:
             continue
         key, val = m.groups()
-        if key == ".name" and not val.endswith(".kd"):
-            cur = {"kernel": val}
-            out.append(cur)
-        elif cur is not None and key in FIELDS:
+        if key == ".name" and not val.endswith(".kd") and line.startswith("    .name"):
+            cur["kernel"] = val
+        elif key in FIELDS and not line.startswith("      "):
             cur[FIELDS[key]] = int(val)
+    out = [k for k in out if "kernel" in k]
     for k in out:
         # gfx950: 512 unified VGPR+AGPR entries per lane per SIMD, allocated in granules of 8; the metadata's
         # .vgpr_count is already the unified total (ArchVGPRs aligned + AGPRs), .agpr_count its AGPR part
