@@ -53,6 +53,21 @@ def gen_sigs(ctx, sk_bytes_list, msgs):
     return sigs
 
 
+def message_variant(ctx, w, v):
+    """Workload variant v: the same sets, keys and jobs with every message replaced (msg key k -> msg_j(v << 24 |
+    k)) and the signatures re-made on the GPU.  Each in-flight step uses its own variant, so no two calls a
+    runtime slot merges into one pipeline run share a signing root: the per-run message dedupe cannot skip
+    hash_to_G2 or Miller-line work that a stream of distinct calls would have to do."""
+    if v == 0:
+        return w
+    msgs = [msg_j((v << 24) | k) for k in w["_mkey"]]
+    sigs = gen_sigs(ctx, w["_sk"], [msg_j((v << 24) | k) for k in w["_skey"]])
+    out = dict(w)
+    out["msgs"] = np.frombuffer(b"".join(msgs), np.uint8)
+    out["sigs"] = np.frombuffer(sigs, np.uint8)
+    return out
+
+
 def build_workload(ctx, config, rank, world=1, n_dev=1):
     """Returns dict of numpy inputs for verify_raw + description.  n_dev > 1: one call spans n_dev in-process
     devices (the runtime shards it), so C2 carries 16,384 sets per device."""
@@ -60,9 +75,11 @@ def build_workload(ctx, config, rank, world=1, n_dev=1):
         n = 16384 * n_dev
         sks, pks = gen_keys(ctx, n)
         ctx.upload_pubkeys(0, pks)
-        msgs = [msg_j(rank * n + j) for j in range(n)]
-        sigs = gen_sigs(ctx, [sks[32 * i : 32 * i + 32] for i in range(n)], msgs)
-        w = dict(job_first_set=np.arange(n + 1, dtype=np.uint32), sigs=np.frombuffer(sigs, np.uint8),
+        mkeys = [rank * n + j for j in range(n)]
+        msgs = [msg_j(k) for k in mkeys]
+        sk_list = [sks[32 * i : 32 * i + 32] for i in range(n)]
+        sigs = gen_sigs(ctx, sk_list, msgs)
+        w = dict(_sk=sk_list, _mkey=mkeys, _skey=mkeys,job_first_set=np.arange(n + 1, dtype=np.uint32), sigs=np.frombuffer(sigs, np.uint8),
                  sig_len=np.full(n, 96, np.uint32), msgs=np.frombuffer(b"".join(msgs), np.uint8),
                  set_pk_first=np.arange(n + 1, dtype=np.uint32), pk_index=np.arange(n, dtype=np.uint32),
                  job_flags=np.ones(n, np.uint8), sig_stride=96, pks_table=pks)
@@ -75,13 +92,14 @@ def build_workload(ctx, config, rank, world=1, n_dev=1):
         n_keys = 65536
         sks, pks = gen_keys(ctx, n_keys)
         ctx.upload_pubkeys(0, pks)
-        msgs = [msg_j(rank * n + j) for j in range(n)]
+        mkeys = [rank * n + j for j in range(n)]
+        msgs = [msg_j(k) for k in mkeys]
         agg_sks = []
         for j in range(n):
             s = sum(interop_sk(i) for i in range(512 * j, 512 * j + k)) % R_ORDER
             agg_sks.append(s.to_bytes(32, "big"))
         sigs = gen_sigs(ctx, agg_sks, msgs)
-        w = dict(job_first_set=np.array([0, n], np.uint32), sigs=np.frombuffer(sigs, np.uint8),
+        w = dict(_sk=agg_sks, _mkey=mkeys, _skey=mkeys,job_first_set=np.array([0, n], np.uint32), sigs=np.frombuffer(sigs, np.uint8),
                  sig_len=np.full(n, 96, np.uint32), msgs=np.frombuffer(b"".join(msgs), np.uint8),
                  set_pk_first=np.arange(0, n * k + 1, k, dtype=np.uint32),
                  pk_index=np.arange(n * k, dtype=np.uint32), job_flags=np.zeros(1, np.uint8), sig_stride=96)
@@ -95,14 +113,17 @@ def build_workload(ctx, config, rank, world=1, n_dev=1):
     raise SystemExit(f"unknown config {config}")
 
 
-def _table_workload(ctx, set_idx, set_msg, set_sk, job_sizes, job_flags):
-    """Inputs for a table-mode call: set_idx[i] = pubkey indices of set i, set_sk[i] = its signing key."""
-    sigs = gen_sigs(ctx, [s.to_bytes(32, "big") for s in set_sk], set_msg)
+def _table_workload(ctx, set_idx, set_mkey, set_sk, job_sizes, job_flags, sign_mkey=None):
+    """Inputs for a table-mode call: set_idx[i] = pubkey indices of set i, set_sk[i] = its signing key, set i
+    claims message msg_j(set_mkey[i]) and is signed over msg_j(sign_mkey[i]) (default: the claimed one)."""
+    sign_mkey = set_mkey if sign_mkey is None else sign_mkey
+    sk_list = [s.to_bytes(32, "big") for s in set_sk]
+    sigs = gen_sigs(ctx, sk_list, [msg_j(k) for k in sign_mkey])
     n = len(set_idx)
     spf = np.concatenate([[0], np.cumsum([len(x) for x in set_idx])]).astype(np.uint32)
-    return dict(job_first_set=np.concatenate([[0], np.cumsum(job_sizes)]).astype(np.uint32),
+    return dict(_sk=sk_list, _mkey=list(set_mkey), _skey=list(sign_mkey), job_first_set=np.concatenate([[0], np.cumsum(job_sizes)]).astype(np.uint32),
                 sigs=np.frombuffer(sigs, np.uint8), sig_len=np.full(n, 96, np.uint32),
-                msgs=np.frombuffer(b"".join(set_msg), np.uint8), set_pk_first=spf,
+                msgs=np.frombuffer(b"".join(msg_j(k) for k in set_mkey), np.uint8), set_pk_first=spf,
                 pk_index=np.concatenate([np.asarray(x, np.uint32) for x in set_idx]),
                 job_flags=np.asarray(job_flags, np.uint8), sig_stride=96)
 
@@ -136,7 +157,7 @@ def build_c4(ctx, rank, world):
             continue
         idx = members[~drop] if (~drop).any() else members[:1]
         set_idx.append(idx)
-        set_msg.append(msg_j(c))
+        set_msg.append(c)
         set_sk.append(sum(sk_all[int(i) % 4096] for i in idx) % R_ORDER)
     n = len(set_idx)
     w = _table_workload(ctx, set_idx, set_msg, set_sk, [1] * n, [1] * n)
@@ -169,19 +190,17 @@ def build_c5(ctx, rank):
             idx = rng.choice(n_keys, size=int(rng.integers(1, 129)), replace=False)
         else:
             idx = rng.choice(n_keys, size=512, replace=False)
-        m = msg_j(rank * n + s)
         set_idx.append(idx.astype(np.uint32))
-        set_msg.append(m)
+        set_msg.append(rank * n + s)
         set_sk.append(sum(sks[int(i)] for i in idx) % R_ORDER)
-    sign_msgs = [msg_j(rank * n + s + 1_000_000) if s in bad else set_msg[s] for s in range(n)]
+    sign_keys = [rank * n + s + 1_000_000 if s in bad else set_msg[s] for s in range(n)]
     job_sizes = []
     left = n
     while left:
         k = min(left, int(rng.integers(1, 4)))
         job_sizes.append(k)
         left -= k
-    w = _table_workload(ctx, set_idx, sign_msgs, set_sk, job_sizes, [1] * len(job_sizes))
-    w["msgs"] = np.frombuffer(b"".join(set_msg), np.uint8)
+    w = _table_workload(ctx, set_idx, set_msg, set_sk, job_sizes, [1] * len(job_sizes), sign_mkey=sign_keys)
     jfs = w["job_first_set"]
     w["expected"] = np.array([0 if any(s in bad for s in range(jfs[j], jfs[j + 1])) else 1
                               for j in range(len(job_sizes))], np.int8)
@@ -189,6 +208,13 @@ def build_c5(ctx, rank):
             "sets_per_step_per_gpu": n, "pubkeys_per_set": float(np.mean([len(x) for x in set_idx])),
             "pk_mode": "device table (8192 keys)", "invalid_sets": len(bad), "jobs": len(job_sizes)}
     return w, n, desc, int(round(desc["pubkeys_per_set"]))
+
+
+def miller_k_of(st):
+    """Pairings per Miller accumulator a run used (the runtime picks it by run size when miller_k = 0): the
+    op-count key (1, 2, 4, 8) nearest to pairing units / Miller chunks."""
+    k = st.pairing_units / max(st.miller_chunks, 1)
+    return min((1, 2, 4, 8), key=lambda c: abs(np.log2(c) - np.log2(max(k, 1.0))))
 
 
 def stage_mults(n_sets, group_count, pubkeys_per_set, miller_k=2, n_messages=None):
@@ -229,8 +255,8 @@ def roofline(runs, n_sets, group_count, pubkeys_per_set, sets_per_s, miller_k=2,
     prod = np.zeros(len(STAGES))
     ms = np.zeros(len(STAGES))
     ppm = 288
-    for st_ms, rs, g, nm in runs:
-        mults, ppm = stage_mults(rs, g, pubkeys_per_set, miller_k, nm)
+    for st_ms, rs, g, nm, mk in runs:
+        mults, ppm = stage_mults(rs, g, pubkeys_per_set, mk, nm)
         prod += np.array([mults[k] for k in STAGES]) * ppm
         ms += np.array(st_ms[:len(STAGES)])
     best = int(np.argmax(ms))
@@ -239,8 +265,16 @@ def roofline(runs, n_sets, group_count, pubkeys_per_set, sets_per_s, miller_k=2,
     per_stage = {STAGES[k]: {"ms_per_launch": round(ms[k] / n_runs, 4),
                              "tproducts_per_s": round(prod[k] / max(ms[k] * 1e-3, 1e-12) / 1e12, 3)}
                  for k in range(len(STAGES))}
-    mults1, ppm = stage_mults(n_sets, group_count, pubkeys_per_set, miller_k, n_messages)
-    pipe = sum(mults1.values()) * ppm / n_sets * sets_per_s
+    # whole chip: the algorithmic products of the timed runs per set they verified (each run priced with the
+    # miller_k it used), at the measured sets/s
+    run_sets = sum(r[1] for r in runs)
+    if run_sets:
+        pipe = float(prod.sum()) / run_sets * sets_per_s
+        per_set_products = float(prod.sum()) / run_sets
+    else:
+        mults1, ppm = stage_mults(n_sets, group_count, pubkeys_per_set, miller_k, n_messages)
+        per_set_products = sum(mults1.values()) * ppm / n_sets
+        pipe = per_set_products * sets_per_s
     out = {
         "bound": "valu-int",
         "kernel": KERNEL_OF_STAGE[best],
@@ -253,7 +287,7 @@ def roofline(runs, n_sets, group_count, pubkeys_per_set, sets_per_s, miller_k=2,
         "sets_per_launch": round(float(np.mean([r[1] for r in runs])), 1) if runs else 0,
         "algorithmic_products_per_launch": round(prod[best] / n_runs),
         "avg_launch_ms": round(ms[best] / n_runs, 4),
-        "pipeline_products_per_set": round(sum(mults1.values()) * ppm / n_sets),
+        "pipeline_products_per_set": round(per_set_products),
         "pipeline_achieved": round(pipe / 1e12, 4),
         "pipeline_frac": round(pipe / VALU_PEAK_PRODUCTS, 5),
         "stages": per_stage,
@@ -328,14 +362,15 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
-    ap.add_argument("--group-sets", type=int, default=256)
+    ap.add_argument("--group-sets", type=int, default=1024)
     ap.add_argument("--inflight", type=int, default=32,
                     help="verifySignatureSets calls in flight per GPU (runtime slots); 1 = strictly serial")
     ap.add_argument("--slots", type=int, default=4,
                     help="runtime slots per GPU (0 = one per in-flight call); fewer slots than calls in flight make "
                          "each slot merge the queued calls into one pipeline run")
     ap.add_argument("--merge-sets", type=int, default=131072, help="max sets of one merged pipeline run (0 = never)")
-    ap.add_argument("--miller-k", type=int, default=2, help="pairings per Miller accumulator (shared squarings)")
+    ap.add_argument("--miller-k", type=int, default=0,
+                    help="pairings per Miller accumulator (shared squarings); 0 = the runtime's choice by run size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
@@ -371,15 +406,21 @@ def main():
     ctx.set_option("merge_sets", args.merge_sets)
     ctx.set_option("miller_k", args.miller_k)
     work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev)
-    call = dict(work)
-    expected = call.pop("expected", None)
-    call.pop("pks_table", None)
+    expected = work.pop("expected", None)
     if expected is None:
-        expected = np.ones(len(call["job_first_set"]) - 1, np.int8)
+        expected = np.ones(len(work["job_first_set"]) - 1, np.int8)
+    # one message variant per in-flight call (step i uses variant i mod V, V > calls in flight)
+    n_var = max(2, args.inflight + 1)
+    t_gen = time.perf_counter()
+    variants = [message_variant(ctx, work, v) for v in range(n_var)]
+    t_gen = time.perf_counter() - t_gen
+    strip = lambda w: {k: v for k, v in w.items() if not k.startswith("_") and k != "pks_table"}
+    calls = [strip(w) for w in variants]
+    call = calls[0]
 
-    def step(_=None):
+    def step(i=0):
         t1 = time.perf_counter()
-        res, st = ctx.verify_raw(**call, seed=SEED)
+        res, st = ctx.verify_raw(**calls[i % n_var], seed=SEED)
         lat_ms = (time.perf_counter() - t1) * 1e3
         if not np.array_equal(res, expected):
             bad = np.nonzero(res != expected)[0]
@@ -390,6 +431,7 @@ def main():
     pool = ThreadPoolExecutor(max_workers=max(1, args.inflight))  # ctypes releases the GIL inside the call
     for _ in range(args.warmup):
         list(pool.map(step, range(max(1, args.inflight))))
+    # the untimed isolated calls below use variant 0
 
     def barrier():
         if dist is not None:
@@ -430,7 +472,7 @@ def main():
     groups, n_msgs = st_iso.groups, st_iso.unique_messages  # one call alone: its own groups / distinct messages
     out = {
         "metric": "verified signature sets/sec (node)",
-        "miller_k": args.miller_k,
+        "miller_k": args.miller_k or "auto",
         "value": round(value, 2),
         "unit": "sets/s",
         "n_gpus": n_gpus,
@@ -441,7 +483,8 @@ def main():
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u32/u64 (28-bit-limb Montgomery integer arithmetic)",
-        "data": "synthetic (interop keys, SHA-256 messages, signatures generated on the GPU before timing)",
+        "data": f"synthetic (interop keys, SHA-256 messages, signatures generated on the GPU before timing; "
+                f"{n_var} message variants, one per in-flight call, so merged runs share no signing root)",
         "config": dict(desc, group_sets=args.group_sets, batch_groups_per_step=groups, inflight=args.inflight,
                        slots=args.slots or args.inflight, merge_sets=args.merge_sets,
                        parallelism=f"shard-by-job x{n_gpus} ({'one process per GPU' if world > 1 else 'in-process devices'}), no collective"),
@@ -450,18 +493,20 @@ def main():
                                        "p99": round(float(np.percentile(call_lat, 99)), 2)},
     }
     if not args.no_profile:
-        runs = [(list(st.stage_ms[:8]), st.run_sets, st.groups, st.unique_messages // n_dev) for st in stats
-                if st.run_sets > 0 and n_dev == 1]
+        runs = [(list(st.stage_ms[:8]), st.run_sets, st.groups, st.unique_messages // n_dev, miller_k_of(st))
+                for st in stats if st.run_sets > 0 and n_dev == 1]
         ctx.set_option("profile", 1)
         stage_acc = np.zeros(8)
         for _ in range(2):
-            stage_acc += np.array(step()[0].stage_ms[:8])
+            st_p = step()[0]
+            stage_acc += np.array(st_p.stage_ms[:8])
         ctx.set_option("profile", 0)
         out["roofline"] = roofline(runs, n_sets // n_dev, groups // n_dev, pk_per_set, value / n_gpus,
-                                   args.miller_k, n_msgs // n_dev, isolated=stage_acc / 2)
+                                   miller_k_of(st_p), n_msgs // n_dev, isolated=stage_acc / 2)
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(dict(call, pks_table=work["pks_table"]) if "pks_table" in work else call,
                                            expected)
+    out["workload_variants"] = {"count": n_var, "gen_s": round(t_gen, 2)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     pool.shutdown()

@@ -136,10 +136,11 @@ typedef void (*blsgpu_done_cb)(void* user, int status);
 int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result, blsgpu_stats* stats,
                   blsgpu_done_cb done, void* user);
 
-/* Tunables: "group_sets" (sets per batch group before a new one opens, default 256), "slots" (runtime slots
+/* Tunables: "group_sets" (sets per batch group before a new one opens, default 1024), "slots" (runtime slots
  * per device, only grows, default 4), "max_devices" (devices one call may shard over, default all),
  * "dedupe" (message dedupe + same-message pairing, 0/1, default 1), "miller_k" (pairings per Miller
- * accumulator sharing its Fp12 squarings, 1..64, default 2), "merge_sets" (a runtime slot merges calls
+ * accumulator sharing its Fp12 squarings, 1..64; default 0 = by run size: 1 below 32768 sets, 2 below 65536,
+ * else 4), "merge_sets" (a runtime slot merges calls
  * already queued on its device into one pipeline run of up to this many sets -- jobs and results stay per
  * call -- default 65536, 0 = never), "profile" (per-stage kernel times in
  * blsgpu_stats.stage_ms, 0/1).  Applies to calls submitted afterwards. */

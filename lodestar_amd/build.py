@@ -21,6 +21,22 @@ SOURCES = ["k_sig.hip", "k_msm.hip", "k_hash.hip", "k_pk.hip", "k_miller.hip", "
 OBJ_DIR = os.path.join(PKG, "build")  # per-TU objects, kept so an edit rebuilds only the TUs it touches
 
 
+# Per-translation-unit defines of the product build.  BLSGPU_TU_DEFINES overrides it for experiments:
+# "k_miller.hip=BLS_INLINE_PRODUCTS=1+OTHER=2;k_hash.hip=..." ("" = none).
+TU_DEFINES = {}
+
+
+def tu_defines():
+    env = os.environ.get("BLSGPU_TU_DEFINES")
+    if env is None:
+        return TU_DEFINES
+    out = {}
+    for part in filter(None, env.split(";")):
+        tu, _, defs = part.partition("=")
+        out[tu] = [d for d in defs.split("+") if d]
+    return out
+
+
 def _headers():
     out = [os.path.join(ROOT, "include", "blsgpu.h")]
     for f in os.listdir(CSRC):
@@ -56,6 +72,7 @@ def build(force=False, verbose=True):
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include")]
     defines = os.environ.get("BLSGPU_DEFINES", "").split()  # e.g. BLSGPU_WPE=2
     common += ["-D" + d for d in defines]
+    tu_defs = tu_defines()
     os.makedirs(OBJ_DIR, exist_ok=True)
     # objects are keyed by the library name and the defines, so variant builds never reuse each other's objects
     key = os.path.splitext(os.path.basename(LIB))[0] + ("." + "_".join(defines).replace("=", "-") if defines else "")
@@ -63,11 +80,13 @@ def build(force=False, verbose=True):
     procs = []
     t0 = time.time()
     for src in SOURCES:
-        obj = os.path.join(OBJ_DIR, key + "." + os.path.splitext(src)[0] + ".o")
+        tdefs = tu_defs.get(src, [])
+        obj = os.path.join(OBJ_DIR, key + "." + os.path.splitext(src)[0] +
+                           ("." + "_".join(tdefs).replace("=", "-") if tdefs else "") + ".o")
         objs.append(obj)
         if not force and os.path.exists(obj) and all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in _tu_deps(src)):
             continue
-        cmd = [HIPCC] + common + ["-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [HIPCC] + common + ["-D" + d for d in tdefs] + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append((src, subprocess.Popen(cmd)))

@@ -20,7 +20,7 @@ def ctx():
 
 
 def run(ctx, w, seed=bench.SEED, **over):
-    call = {k: v for k, v in w.items() if k not in ("expected", "pks_table")}
+    call = {k: v for k, v in w.items() if k not in ("expected", "pks_table") and not k.startswith("_")}
     call.update(over)
     res, st = ctx.verify_raw(**call, seed=seed)
     return res, st
@@ -37,6 +37,11 @@ def test_c5_mixed_one_percent_invalid(ctx):
     assert np.array_equal(res2, w["expected"])
     res3, _ = run(ctx, w, job_flags=np.zeros(len(w["expected"]), np.uint8))
     assert np.array_equal(res3, w["expected"])
+    # a message variant of the bench's in-flight pool (new roots, re-signed): the same per-job answers
+    w1 = bench.message_variant(ctx, w, 3)
+    assert not np.array_equal(w1["msgs"], w["msgs"])
+    res4, _ = run(ctx, w1)
+    assert np.array_equal(res4, w["expected"])
 
 
 def test_c3_block_import_aggregates(ctx):
