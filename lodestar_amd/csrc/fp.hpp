@@ -65,10 +65,12 @@ struct fp2 {
 // Host-only instrumentation (tests/native/emu.cpp with -DBLS_COUNT_OPS): counts Montgomery
 // multiplications / squarings of the device algorithm to give the roofline its algorithmic work.
 #if defined(BLS_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
-extern unsigned long long bls_count_mul, bls_count_sqr;
+extern unsigned long long bls_count_mul, bls_count_sqr, bls_count_half;
 #define BLS_COUNT(x) (x++)
+#define BLS_COUNT5(x) (x += 5)
 #else
 #define BLS_COUNT(x) ((void)0)
+#define BLS_COUNT5(x) ((void)0)
 #endif
 
 // ------------------------------------------------------------------------------------------------

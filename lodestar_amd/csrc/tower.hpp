@@ -27,20 +27,184 @@ BLS_HD fp2 fp2_half(const fp2& a) { return fp2_make(fp_half(a.c0), fp_half(a.c1)
 BLS_HD fp2 fp2_conj(const fp2& a) { return fp2_make(a.c0, fp_neg(a.c1)); }
 BLS_HD fp2 fp2_add_nr(const fp2& a, const fp2& b) { return fp2_make(fp_add_nr(a.c0, b.c0), fp_add_nr(a.c1, b.c1)); }
 
+// 64 p^2 in 28 limbs of 28 bits: the multiple of p added to a0 b0 - a1 b1 in fp2_mul_lazy_body so the c0 column sum
+// stays a non-negative integer for inputs < 8p (a1 b1 < 64 p^2)
+BLS_CONST uint32_t FP2_LAZY_OFS[2 * BLS_NL] = {
+    0xc638e40, 0x8000071, 0xbaac9aa, 0xc75d8e0, 0xf5f3b5a, 0xd8844f3, 0x58b0ce0, 0x9c6dd0c, 0xfe47b4f, 0x681259a,
+    0x16a1c24, 0x1eca4ba, 0x7218617, 0x475a186, 0x25e3bc0, 0x4c524cc, 0x7729bbd, 0x8b3f45b, 0x2f41429, 0x924d27a,
+    0xd19b967, 0x439c11a, 0x8b72439, 0x8bc97a7, 0x49e3aa8, 0xd7f1d2f, 0xde92e30, 0x0000a90};
+
+// Fp2 product with lazy reduction: ONE Montgomery reduction per output coefficient, the three half-products
+// (a0 b0, a1 b1, (a0 + a1)(b0 + b1), column sums only) interleaved column by column:
+//   c0 = Redc(a0 b0 - a1 b1 + 64 p^2),   c1 = Redc((a0 + a1)(b0 + b1) - a0 b0 - a1 b1)
+// 5 x 196 = 980 v_mad_u64_u32 instead of 3 x 392, and five independent MAD chains per column instead of one.
+// Inputs: limbs < 2^29 (normalized values or one fp_add_nr level), values < 8p.  Column bounds: t0, t1 < 14 * 2^58,
+// t2 < 14 * 2^60 (the limb sums a0_i + a1_i < 2^30 are not normalized); t2 - t0 - t1 is exactly the cross-term
+// column sum(a0_i b1_j + a1_i b0_j) >= 0; t0 - t1 + ofs may be negative, so c0 runs on a signed accumulator with
+// arithmetic shifts (|acc0| < 2^63).  Outputs: normalized limbs, values < 1.06 p.
+BLS_INL fp2 fp2_mul_lazy_body(const fp& a0, const fp& a1, const fp& b0, const fp& b1) {
+  uint32_t s[BLS_NL], u[BLS_NL], m0[BLS_NL], m1[BLS_NL];
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    s[i] = a0.l[i] + a1.l[i];
+    u[i] = b0.l[i] + b1.l[i];
+  }
+  int64_t acc0 = 0;
+  uint64_t acc1 = 0;
+  fp2 r;
+#pragma unroll
+  for (int k = 0; k < 2 * BLS_NL - 1; k++) {
+    const int lo = k < BLS_NL ? 0 : k - BLS_NL + 1, hi = k < BLS_NL ? k : BLS_NL - 1;
+    uint64_t t0 = 0, t1 = 0, t2 = 0;
+#pragma unroll
+    for (int i = lo; i <= hi; i++) {
+      t0 += (uint64_t)a0.l[i] * b0.l[k - i];
+      t1 += (uint64_t)a1.l[i] * b1.l[k - i];
+      t2 += (uint64_t)s[i] * u[k - i];
+    }
+    acc0 += (int64_t)(t0 - t1) + (int64_t)FP2_LAZY_OFS[k];
+    acc1 += t2 - t0 - t1;
+    const int mhi = k < BLS_NL ? k - 1 : BLS_NL - 1;
+#pragma unroll
+    for (int i = lo; i <= mhi; i++) {
+      acc0 += (int64_t)((uint64_t)m0[i] * FP_P.l[k - i]);
+      acc1 += (uint64_t)m1[i] * FP_P.l[k - i];
+    }
+    if (k < BLS_NL) {
+      const uint32_t q0 = ((uint32_t)acc0 * BLS_N0INV) & BLS_MASK, q1 = ((uint32_t)acc1 * BLS_N0INV) & BLS_MASK;
+      m0[k] = q0;
+      m1[k] = q1;
+      acc0 += (int64_t)((uint64_t)q0 * FP_P.l[0]);
+      acc1 += (uint64_t)q1 * FP_P.l[0];
+    } else {
+      r.c0.l[k - BLS_NL] = (uint32_t)acc0 & BLS_MASK;
+      r.c1.l[k - BLS_NL] = (uint32_t)acc1 & BLS_MASK;
+    }
+    acc0 >>= BLS_LB;  // arithmetic: the low 28 bits are zero (k < 14) or emitted
+    acc1 >>= BLS_LB;
+  }
+  r.c0.l[BLS_NL - 1] = (uint32_t)(acc0 + (int64_t)FP2_LAZY_OFS[2 * BLS_NL - 1]);
+  r.c1.l[BLS_NL - 1] = (uint32_t)acc1;
+  return r;
+}
+
+// Fp2 squaring (complex method): c0 = (a0 + a1)(a0 - a1), c1 = 2 a0 a1 -- two independent products.
+BLS_INL fp2 fp2_sqr_body(const fp2& a) {
+  const fp c0 = fp_mul_body(fp_add_nr(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  const fp c1 = fp_mul_body(fp_add_nr(a.c0, a.c0), a.c1);
+  return fp2_make(c0, c1);
+}
+
+// Device call boundary of the Fp2 products (fp.hpp "call-granularity policy"):
+//   fp2_mul: ONE call running the lazy-reduction body (five interleaved MAD chains).  The AMDGPU calling
+//            convention passes only 32 VGPR arguments in registers, so a0, a1 go as the 28 register arguments and
+//            b0, b1 through a per-lane LDS slot (word-major: lane t, word w at bls_fp2_arg[w * 128 + t],
+//            conflict-free; every kernel that reaches it has <= 128 lanes per workgroup);
+//   fp2_sqr: ONE register-ABI call computing its two products interleaved.
+// tools/microbench/fp2_rate.hip (profiles/r02_fp2_rate.json): 1.85e10 Fp2 products/s per chip at one wave per
+// SIMD with this call vs 1.39e10 for three fp_mul_r calls.
+#if defined(__HIP_DEVICE_COMPILE__) && !BLS_INLINE_PRODUCTS && !BLS_FP2_CLASSIC
+#define BLS_FP2_LDS_LANES 128
+__shared__ uint32_t bls_fp2_arg[2 * BLS_NL * BLS_FP2_LDS_LANES];
+struct fp2_ret {
+  uint32_t l[2 * BLS_NL];
+};
+__device__ __noinline__ fp2_ret fp2_mul_r(BLS_PARAMS14(a), BLS_PARAMS14(c)) {
+  const fp x0 = BLS_INIT14(a), x1 = BLS_INIT14(c);
+  const uint32_t t = threadIdx.x;
+  fp y0, y1;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    y0.l[i] = bls_fp2_arg[i * BLS_FP2_LDS_LANES + t];
+    y1.l[i] = bls_fp2_arg[(BLS_NL + i) * BLS_FP2_LDS_LANES + t];
+  }
+  const fp2 r = fp2_mul_lazy_body(x0, x1, y0, y1);
+  fp2_ret o;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    o.l[i] = r.c0.l[i];
+    o.l[BLS_NL + i] = r.c1.l[i];
+  }
+  return o;
+}
+__device__ __noinline__ fp2_ret fp2_sqr_r(BLS_PARAMS14(a), BLS_PARAMS14(c)) {
+  const fp2 r = fp2_sqr_body(fp2_make(BLS_INIT14(a), BLS_INIT14(c)));
+  fp2_ret o;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    o.l[i] = r.c0.l[i];
+    o.l[BLS_NL + i] = r.c1.l[i];
+  }
+  return o;
+}
+__device__ __forceinline__ fp2 fp2_from_ret(const fp2_ret& o) {
+  fp2 r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    r.c0.l[i] = o.l[i];
+    r.c1.l[i] = o.l[BLS_NL + i];
+  }
+  return r;
+}
+__device__ __forceinline__ fp2 fp2_mul(const fp2& a, const fp2& b) {
+  const uint32_t t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    bls_fp2_arg[i * BLS_FP2_LDS_LANES + t] = b.c0.l[i];
+    bls_fp2_arg[(BLS_NL + i) * BLS_FP2_LDS_LANES + t] = b.c1.l[i];
+  }
+  return fp2_from_ret(fp2_mul_r(BLS_ARGS14(a.c0), BLS_ARGS14(a.c1)));
+}
+__device__ __forceinline__ fp2 fp2_sqr(const fp2& a) { return fp2_from_ret(fp2_sqr_r(BLS_ARGS14(a.c0), BLS_ARGS14(a.c1))); }
+// a * s (s in Fp, through the LDS slot): two interleaved products in one call
+__device__ __noinline__ fp2_ret fp2_mul_fp_r(BLS_PARAMS14(a), BLS_PARAMS14(c)) {
+  const fp x0 = BLS_INIT14(a), x1 = BLS_INIT14(c);
+  const uint32_t t = threadIdx.x;
+  fp y;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) y.l[i] = bls_fp2_arg[i * BLS_FP2_LDS_LANES + t];
+  const fp r0 = fp_mul_body(x0, y), r1 = fp_mul_body(x1, y);
+  fp2_ret o;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    o.l[i] = r0.l[i];
+    o.l[BLS_NL + i] = r1.l[i];
+  }
+  return o;
+}
+__device__ __forceinline__ fp2 fp2_mul_fp(const fp2& a, const fp& s) {
+  const uint32_t t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) bls_fp2_arg[i * BLS_FP2_LDS_LANES + t] = s.l[i];
+  return fp2_from_ret(fp2_mul_fp_r(BLS_ARGS14(a.c0), BLS_ARGS14(a.c1)));
+}
+#elif BLS_FP2_CLASSIC
+// A/B reference (BLSGPU_DEFINES=BLS_FP2_CLASSIC=1): three / two separate product calls, eager reduction
+BLS_FN fp2 fp2_mul_fp(const fp2& a, const fp& s) { return fp2_make(fp_mul(a.c0, s), fp_mul(a.c1, s)); }
 BLS_FN fp2 fp2_mul(const fp2& a, const fp2& b) {
   fp t0 = fp_mul(a.c0, b.c0);
   fp t1 = fp_mul(a.c1, b.c1);
   fp t2 = fp_mul(fp_add_nr(a.c0, a.c1), fp_add_nr(b.c0, b.c1));
   return fp2_make(fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1));
 }
-
 BLS_FN fp2 fp2_sqr(const fp2& a) {
   fp c0 = fp_mul(fp_add_nr(a.c0, a.c1), fp_sub(a.c0, a.c1));
   fp c1 = fp_mul(fp_add_nr(a.c0, a.c0), a.c1);
   return fp2_make(c0, c1);
 }
-
+#else
 BLS_FN fp2 fp2_mul_fp(const fp2& a, const fp& s) { return fp2_make(fp_mul(a.c0, s), fp_mul(a.c1, s)); }
+BLS_FN fp2 fp2_mul(const fp2& a, const fp2& b) {
+  BLS_COUNT5(bls_count_half);  // 3 half-products + 2 reductions, each half a Montgomery multiplication
+  return fp2_mul_lazy_body(a.c0, a.c1, b.c0, b.c1);
+}
+BLS_FN fp2 fp2_sqr(const fp2& a) {
+  BLS_COUNT(bls_count_mul);
+  BLS_COUNT(bls_count_mul);
+  return fp2_sqr_body(a);
+}
+#endif
+
 
 // (a0 + a1 u)(1 + u) = (a0 - a1) + (a0 + a1) u
 BLS_FN fp2 fp2_mul_xi(const fp2& a) { return fp2_make(fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)); }

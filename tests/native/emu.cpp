@@ -6,7 +6,7 @@
 #include "../../lodestar_amd/csrc/msm.hpp"
 
 #if defined(BLS_COUNT_OPS)
-unsigned long long bls_count_mul = 0, bls_count_sqr = 0;
+unsigned long long bls_count_mul = 0, bls_count_sqr = 0, bls_count_half = 0;
 #endif
 
 static fp load_mont(const uint8_t* b) {
@@ -115,11 +115,12 @@ void emu_stage_sig_msm(const uint8_t* pts192, int n) {
     z = z * 6364136223846793005ull + 1442695040888963407ull;
     w[i] = z;
   }
-  bls_count_mul = bls_count_sqr = 0;
+  bls_count_mul = bls_count_sqr = bls_count_half = 0;
   (void)emu_msm_core(P, w, nullptr, n);
 }
-void emu_count_reset() { bls_count_mul = bls_count_sqr = 0; }
-unsigned long long emu_count_mul() { return bls_count_mul; }
+void emu_count_reset() { bls_count_mul = bls_count_sqr = bls_count_half = 0; }
+// lazy-reduction Fp2 products count half-products and reductions (each half a multiplication): reported in mul
+unsigned long long emu_count_mul() { return bls_count_mul + bls_count_half / 2; }
 unsigned long long emu_count_sqr() { return bls_count_sqr; }
 // kernel-shaped stages (same calls as kernels.hip)
 void emu_stage_sig_scale(const uint8_t* sig192, uint64_t r) { (void)jac_mul_u64(load_g2(sig192), r); }
@@ -296,4 +297,23 @@ void emu_fp12_sqr(const uint8_t* a, uint8_t* out) { store12(fp12_sqr(load12(a)),
 void emu_fp12_inv(const uint8_t* a, uint8_t* out) { store12(fp12_inv(load12(a)), out); }
 void emu_fp12_cyc_sqr(const uint8_t* a, uint8_t* out) { store12(fp12_cyclotomic_sqr(load12(a)), out); }
 void emu_fp12_frob1(const uint8_t* a, uint8_t* out) { store12(fp12_frob1(load12(a)), out); }
+}
+extern "C" void emu_fp2_mul_lazy(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  const fp2 x = load2(a), y = load2(b);
+  store2(fp2_mul_lazy_body(x.c0, x.c1, y.c0, y.c1), out);
+}
+// raw-limb entry: a0, a1, b0, b1 as 14 uint32 limbs each (any limb pattern the bounds allow), out 28 limbs
+extern "C" void emu_fp2_mul_lazy_limbs(const uint32_t* in56, uint32_t* out28) {
+  fp a0, a1, b0, b1;
+  for (int i = 0; i < BLS_NL; i++) {
+    a0.l[i] = in56[i];
+    a1.l[i] = in56[14 + i];
+    b0.l[i] = in56[28 + i];
+    b1.l[i] = in56[42 + i];
+  }
+  const fp2 r = fp2_mul_lazy_body(a0, a1, b0, b1);
+  for (int i = 0; i < BLS_NL; i++) {
+    out28[i] = r.c0.l[i];
+    out28[14 + i] = r.c1.l[i];
+  }
 }

@@ -238,3 +238,40 @@ def test_bucket_msm_matches_sum_of_scalings():
             assert got == 0
         else:
             assert got == 1 and b2g2(out.raw) == want, (words, active)
+
+
+def _limbs_of(v, r2):
+    """A 14 x 28-bit limb pattern of the integer v: normalized, or with random borrows moved into the lower
+    limbs so limbs reach up to 2^29 - 1 (the un-normalized operands fp2_mul_lazy_body accepts)."""
+    l = [(v >> (28 * i)) & 0xFFFFFFF for i in range(14)]
+    l[13] = v >> (28 * 13)
+    if r2.random() < 0.5:
+        for i in range(13):
+            if l[i + 1] > 0 and r2.random() < 0.7:
+                l[i + 1] -= 1
+                l[i] += 1 << 28
+    assert sum(x << (28 * i) for i, x in enumerate(l)) == v and all(0 <= x < 2**29 for x in l)
+    return l
+
+
+def test_fp2_mul_lazy_reduction_bounds():
+    """tower.hpp fp2_mul_lazy_body on raw limbs at the edges of its contract (limbs < 2^29, values < 8p):
+    c0 = (a0 b0 - a1 b1) / R and c1 = (a0 b1 + a1 b0) / R mod p, outputs normalized and < 1.06 p."""
+    L = lib()
+    L.emu_fp2_mul_lazy_limbs.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    r2 = random.Random(4242)
+    RINV = pow(2**392, -1, P)
+    edge = [0, 1, P - 1, P, 2 * P, 8 * P - 1, 8 * P - 2**300, 2**383, 2**384 - 1 if 2**384 - 1 < 8 * P else 8 * P - 1]
+    out = (ctypes.c_uint32 * 28)()
+    for it in range(3000):
+        vals = [r2.choice(edge) if r2.random() < 0.3 else r2.randrange(8 * P) for _ in range(4)]
+        limbs = [x for v in vals for x in _limbs_of(v, r2)]
+        L.emu_fp2_mul_lazy_limbs((ctypes.c_uint32 * 56)(*limbs), out)
+        o = list(out)
+        assert all(x < 2**28 for x in o), (vals, o)
+        c0 = sum(x << (28 * i) for i, x in enumerate(o[:14]))
+        c1 = sum(x << (28 * i) for i, x in enumerate(o[14:]))
+        a0, a1, b0, b1 = vals
+        assert c0 < 1.06 * P and c1 < 1.06 * P, (vals,)
+        assert c0 % P == (a0 * b0 - a1 * b1) * RINV % P, (it, vals)
+        assert c1 % P == (a0 * b1 + a1 * b0) * RINV % P, (it, vals)
