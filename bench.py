@@ -54,14 +54,14 @@ def gen_sigs(ctx, sk_bytes_list, msgs):
 
 
 def message_variant(ctx, w, v):
-    """Workload variant v: the same sets, keys and jobs with every message replaced (msg key k -> msg_j(v << 24 |
-    k)) and the signatures re-made on the GPU.  Each in-flight step uses its own variant, so no two calls a
+    """Workload variant v: the same sets, keys and jobs with every message replaced (msg key k -> msg_j(k) under the
+    seed SEED + v) and the signatures re-made on the GPU.  Each in-flight step uses its own variant, so no two calls a
     runtime slot merges into one pipeline run share a signing root: the per-run message dedupe cannot skip
     hash_to_G2 or Miller-line work that a stream of distinct calls would have to do."""
     if v == 0:
         return w
-    msgs = [msg_j((v << 24) | k) for k in w["_mkey"]]
-    sigs = gen_sigs(ctx, w["_sk"], [msg_j((v << 24) | k) for k in w["_skey"]])
+    msgs = [msg_j(k, SEED + v) for k in w["_mkey"]]
+    sigs = gen_sigs(ctx, w["_sk"], [msg_j(k, SEED + v) for k in w["_skey"]])
     out = dict(w)
     out["msgs"] = np.frombuffer(b"".join(msgs), np.uint8)
     out["sigs"] = np.frombuffer(sigs, np.uint8)

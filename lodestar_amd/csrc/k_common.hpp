@@ -15,6 +15,27 @@
 #define BLSGPU_WPE 1
 #endif
 #define STAGE_KERNEL __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(BLSGPU_WPE, BLSGPU_WPE)))
+// Per-kernel register budgets (waves per SIMD), default BLSGPU_WPE: a kernel whose live state fits 256 registers
+// with little spilling can take two waves per SIMD, so two waves hide each other's dependent-MAD latency.
+#define STAGE_KERNEL_W(w) __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(w, w)))
+#ifndef BLSGPU_WPE_PK
+#define BLSGPU_WPE_PK BLSGPU_WPE
+#endif
+#ifndef BLSGPU_WPE_MSM
+#define BLSGPU_WPE_MSM BLSGPU_WPE
+#endif
+#ifndef BLSGPU_WPE_LINES
+#define BLSGPU_WPE_LINES BLSGPU_WPE
+#endif
+#ifndef BLSGPU_WPE_ACC
+#define BLSGPU_WPE_ACC BLSGPU_WPE
+#endif
+#ifndef BLSGPU_WPE_DEC
+#define BLSGPU_WPE_DEC BLSGPU_WPE
+#endif
+#ifndef BLSGPU_WPE_HASH
+#define BLSGPU_WPE_HASH BLSGPU_WPE
+#endif
 
 __device__ __forceinline__ fp ld_fp(const uint32_t* p, uint32_t n, uint32_t i, int w0) {
   fp r;

@@ -69,9 +69,10 @@ __global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const 
 // One 128-lane workgroup per group: the Miller loop and the final exponentiation run as cooperative Fp12
 // arithmetic (gt_wave.hpp), one Fp product per lane per step.
 __global__ __launch_bounds__(GTW_LANES) void k_group_check(const uint32_t* S_in, const uint32_t* F_in, uint32_t ng,
-                                                           uint8_t* ok) {
+                                                           const uint32_t* sel, uint8_t* ok) {
   __shared__ GtwLds sh;
-  const uint32_t g = blockIdx.x, t = threadIdx.x;
+  const uint32_t t = threadIdx.x;
+  const uint32_t g = sel ? sel[blockIdx.x] : blockIdx.x;  // entry checked (S_in / F_in stride ng); verdict ok[blockIdx.x]
   // F: SoA tower layout (Fp2 slots c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2) -> LDS w-basis
   for (uint32_t w = t; w < W_FP12; w += GTW_LANES) {
     const uint32_t slot = w / (2 * W_FP), rest = w % (2 * W_FP);
@@ -95,7 +96,41 @@ __global__ __launch_bounds__(GTW_LANES) void k_group_check(const uint32_t* S_in,
     gtw_mul<false>(sh.F, sh.F, sh.G, sh.S, t);
   }
   gtw_final_exp(sh.F, sh.W, sh.S, t);
-  if (t == 0) ok[g] = fp12_is_one(gtw_to_reg(sh.F)) ? 1 : 0;
+  if (t == 0) ok[blockIdx.x] = fp12_is_one(gtw_to_reg(sh.F)) ? 1 : 0;
+}
+
+// Fallback sub-groups: S_out[r] = sum S_in[e], F_out[r] = prod F_in[e] over the entries e of range r
+// (entries = per-job values, stride n_in; one wave per range, strided partials + LDS tree).
+__global__ __launch_bounds__(WAVE) void k_range_combine(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in,
+                                                        const uint32_t* ranges, uint32_t n_out, uint32_t* S_out,
+                                                        uint32_t* F_out) {
+  __shared__ uint32_t red[WAVE * (W_G2J + W_FP12)];
+  const uint32_t r = blockIdx.x, lane = threadIdx.x;
+  if (r >= n_out) return;
+  const uint32_t first = ranges[2 * r], last = ranges[2 * r + 1];
+  g2j S = jac_infinity<fp2>();
+  fp12 F = fp12_one();
+  for (uint32_t e = first + lane; e < last; e += WAVE) {
+    S = jac_add(S, ld_g2j(S_in, n_in, e));
+    F = fp12_mul(F, ld_fp12(F_in, n_in, e));
+  }
+#pragma unroll 1
+  for (int h = WAVE / 2; h >= 1; h >>= 1) {
+    if (lane >= (uint32_t)h && lane < (uint32_t)(2 * h)) {
+      st_g2j(red, WAVE, lane - h, S);
+      st_fp12(red + WAVE * W_G2J, WAVE, lane - h, F);
+    }
+    __syncthreads();
+    if (lane < (uint32_t)h) {
+      S = jac_add(S, ld_g2j(red, WAVE, lane));
+      F = fp12_mul(F, ld_fp12(red + WAVE * W_G2J, WAVE, lane));
+    }
+    __syncthreads();
+  }
+  if (lane == 0) {
+    st_g2j(S_out, n_out, r, S);
+    st_fp12(F_out, n_out, r, F);
+  }
 }
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
@@ -107,6 +142,13 @@ void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, c
                          uint32_t ng, uint32_t* S, uint32_t* F, hipStream_t s) {
   if (ng) hipLaunchKernelGGL(k_group_reduce, dim3(ng), dim3(WAVE), 0, s, b, set_ranges, f_ranges, ng, S, F);
 }
-void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s) {
-  if (ng) hipLaunchKernelGGL(k_group_check, dim3(ng), dim3(GTW_LANES), 0, s, S, F, ng, ok);
+void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s,
+                        const uint32_t* sel, uint32_t n_sel) {
+  const uint32_t n = sel ? n_sel : ng;
+  if (n) hipLaunchKernelGGL(k_group_check, dim3(n), dim3(GTW_LANES), 0, s, S, F, ng, sel, ok);
+}
+void launch_range_combine(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,
+                          uint32_t n_out, uint32_t* S_out, uint32_t* F_out, hipStream_t s) {
+  if (n_out)
+    hipLaunchKernelGGL(k_range_combine, dim3(n_out), dim3(WAVE), 0, s, S_in, F_in, n_in, ranges, n_out, S_out, F_out);
 }

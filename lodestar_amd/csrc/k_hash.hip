@@ -45,7 +45,7 @@ STAGE_KERNEL void k_hash_prep(PipelineBuffers b) {
 }
 
 // inv: 1 / N(d) from the batch inversion; d^-1 = conj(d) / N(d).  Jacobian out (affine conversion batched).
-STAGE_KERNEL void k_hash_map(PipelineBuffers b, const uint32_t* inv) {
+STAGE_KERNEL_W(BLSGPU_WPE_HASH) void k_hash_map(PipelineBuffers b, const uint32_t* inv) {
   uint32_t u = blockIdx.x * WAVE + threadIdx.x;
   if (u >= b.n_umsg) return;
   const h2c_prep h = ld_prep(b.h_prep, b.nm, u);

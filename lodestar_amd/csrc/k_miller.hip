@@ -11,7 +11,7 @@
 // Line traffic is 68 x 84 words = 22.8 KB per message (HBM-cheap next to ~5,200 Montgomery products).
 #include "k_common.hpp"
 
-STAGE_KERNEL void k_miller_lines(PipelineBuffers b) {
+STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_miller_lines(PipelineBuffers b) {
   uint32_t u = blockIdx.x * WAVE + threadIdx.x;
   if (u >= b.n_umsg || (b.mflags[u] & MF_H_INF)) return;
   const g2a Q = ld_g2a(b.h_aff, b.nm, u);
@@ -44,7 +44,7 @@ STAGE_KERNEL void k_miller_lines(PipelineBuffers b) {
 // 63 squarings + 68 K line multiplications instead of K (63 + 68).  UNITS: item u is pairing unit u
 // (P = unit_p[u]); otherwise item i is a set (P = r_i pk_i, only if it enters the batch equation).
 template <bool UNITS>
-STAGE_KERNEL void k_miller_acc(PipelineBuffers b) {
+STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc(PipelineBuffers b) {
   const uint32_t c = blockIdx.x * WAVE + threadIdx.x;
   if (c >= b.n_chunks) return;
   const uint32_t k0 = b.chunk_first[c], k1 = b.chunk_first[c + 1];

@@ -14,7 +14,7 @@
 
 #define MSM_LANES (MSM_WINDOWS * MSM_BUCKETS)
 
-__global__ __launch_bounds__(MSM_LANES) __attribute__((amdgpu_waves_per_eu(BLSGPU_WPE, BLSGPU_WPE))) void k_msm_bucket(
+__global__ __launch_bounds__(MSM_LANES) __attribute__((amdgpu_waves_per_eu(BLSGPU_WPE_MSM, BLSGPU_WPE_MSM))) void k_msm_bucket(
     PipelineBuffers b, const uint32_t* slices, uint32_t n_slices, uint32_t* B) {
   __shared__ uint64_t sw[MSM_SLICE];
   __shared__ uint8_t act[MSM_SLICE];

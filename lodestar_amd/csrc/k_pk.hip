@@ -134,7 +134,7 @@ __device__ __forceinline__ int set_pubkey(const PipelineBuffers& b, uint32_t i, 
 // (status[n, 2n)); the job mask gives them precedence over signature statuses because the reference
 // deserializes pubkeys first (worker.ts:39).  A set with a pubkey error stores the identity (z = 0), which
 // the batch inversion skips.
-STAGE_KERNEL void k_pk_finish(PipelineBuffers b, uint32_t n_sets, int8_t* pk_status) {
+STAGE_KERNEL_W(BLSGPU_WPE_PK) void k_pk_finish(PipelineBuffers b, uint32_t n_sets, int8_t* pk_status) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets) return;
   g1j P;

@@ -2,7 +2,7 @@
 // of the random linear combination (A9), one lane per signature set.
 #include "k_common.hpp"
 
-STAGE_KERNEL void k_sig_decode(PipelineBuffers b, uint32_t n_sets) {
+STAGE_KERNEL_W(BLSGPU_WPE_DEC) void k_sig_decode(PipelineBuffers b, uint32_t n_sets) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets) return;
   uint8_t raw[192];
@@ -23,9 +23,11 @@ STAGE_KERNEL void k_sig_decode(PipelineBuffers b, uint32_t n_sets) {
 }
 
 // r_i sig_i with the batch scalar word (0 = r = 1, CoreVerify); the signed-window table goes to b.scal_tab.
-STAGE_KERNEL void k_sig_scale(PipelineBuffers b, uint32_t n_sets) {
-  uint32_t i = blockIdx.x * WAVE + threadIdx.x;
-  if (i >= n_sets) return;
+// The fallback's path for small jobs (runtime.cpp): a per-set scaling costs less than a bucket MSM per 1-3-set job.
+STAGE_KERNEL void k_sig_scale(PipelineBuffers b, uint32_t n_sets, const uint32_t* list) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  if (q >= n_sets) return;
+  const uint32_t i = list ? list[q] : q;
   g2j R = jac_infinity<fp2>();
   if (b.status[i] == BLS_OK && !(b.flags[i] & SF_SIG_INF)) {
     const g2a s = ld_g2a(b.sig_aff, b.n, i);
@@ -40,6 +42,6 @@ static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 void launch_sig_decode(const PipelineBuffers& b, uint32_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_sig_decode, grid_for(n), dim3(WAVE), 0, s, b, n);
 }
-void launch_sig_scale(const PipelineBuffers& b, uint32_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_sig_scale, grid_for(n), dim3(WAVE), 0, s, b, n);
+void launch_sig_scale(const PipelineBuffers& b, uint32_t n, hipStream_t s, const uint32_t* list) {
+  if (n) hipLaunchKernelGGL(k_sig_scale, grid_for(n), dim3(WAVE), 0, s, b, n, list);
 }

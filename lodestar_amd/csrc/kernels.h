@@ -88,7 +88,8 @@ void launch_pk_finish(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 void launch_batch_inv(const uint32_t* src, uint32_t src_stride, int w0, uint32_t* dst, uint32_t n, hipStream_t s);
 void launch_pk_affine(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 void launch_h_affine(const PipelineBuffers& b, hipStream_t s);
-void launch_sig_scale(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
+// r_i sig_i -> b.rsig for the sets list[0 .. n) (all sets when list is null), G2 window tables in b.scal_tab
+void launch_sig_scale(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s, const uint32_t* list = nullptr);
 // S_r = sum r_i sig_i over the included sets of each range, as a bucket MSM (k_msm.hip, msm.hpp).  Range r is the
 // slices [range_slices[r], range_slices[r+1]); slice s is the sets [slices[2s], slices[2s+1]) (<= MSM_SLICE of
 // them).  B: MSM_BUCKET_WORDS words per slice, W: MSM_WINDOW_WORDS per range; S: W_G2J SoA, stride n_ranges.
@@ -113,7 +114,12 @@ void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s);
 void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
                          uint32_t n_groups, uint32_t* S, uint32_t* F, hipStream_t s);
 // check: ok_g = FinalExp(F_g * MillerLoop(-g1, S_g)) == 1
-void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t n_groups, uint8_t* ok, hipStream_t s);
+// (sel: check only the entries sel[0 .. n_sel), verdict q -> ok[q])
+void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t n_groups, uint8_t* ok, hipStream_t s,
+                        const uint32_t* sel = nullptr, uint32_t n_sel = 0);
+// fallback sub-groups: S_out[r] = sum, F_out[r] = prod of the per-job entries ranges[2r] .. ranges[2r+1]
+void launch_range_combine(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,
+                          uint32_t n_out, uint32_t* S_out, uint32_t* F_out, hipStream_t s);
 // pubkey table upload: decode 96-byte affine encodings into table entries, per-entry status
 void launch_pk_table_fill(const uint8_t* pk96, uint32_t n, uint32_t* table_dst, int8_t* status, hipStream_t s);
 // serialize the per-set aggregate (pk_jac) to 96-byte uncompressed or 48-byte compressed encodings

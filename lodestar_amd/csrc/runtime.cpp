@@ -99,14 +99,14 @@ struct Slot {
   // d_in / h_in: every per-call input packed into one arena (one H2D transfer); d_res / h_res: job errors +
   // group verdicts (one D2H transfer).
   DevBuf<uint8_t> d_in, d_res, d_bytes, d_ok;
-  DevBuf<uint32_t> d_work, d_lines, d_S, d_F, d_list, d_msmB, d_msmW;
+  DevBuf<uint32_t> d_work, d_lines, d_S, d_F, d_list, d_msmB, d_msmW, d_fb;
   HostBuf<uint8_t> h_in, h_res, h_ok;
   HostBuf<uint32_t> h_list;
 
   void release_all() {
     d_in.release(); d_res.release(); d_bytes.release(); d_ok.release();
     d_work.release(); d_lines.release(); d_S.release(); d_F.release(); d_list.release();
-    d_msmB.release(); d_msmW.release();
+    d_msmB.release(); d_msmW.release(); d_fb.release();
     h_in.release(); h_res.release(); h_ok.release(); h_list.release();
   }
 };
@@ -633,24 +633,42 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     }
   }
 
-  // ---- fallback: one parallel launch re-checks every clean job of every failed group -----------------------
-  // Each retried job gets its own set range (S) and its own Miller chunks (its sets, miller_k per chunk).
+  // ---- fallback: every clean job of every failed group gets its own verdict ---------------------------------
+  // The reference re-verifies each job of a failed chunk (worker.ts:76-98).  Here each retried job j gets its
+  // own Miller accumulation (its sets, miller_k per chunk) F_j and its own S_j = sum r_i sig_i -- a bucket MSM for
+  // large jobs, per-set scalings (k_sig_scale) plus a sum when the jobs are small (a 1-3-set job would leave a
+  // 128-lane MSM workgroup idle) -- and then, as group testing:
+  //   level 1: sub-groups of kFbSub consecutive retried jobs are checked with one final exponentiation each
+  //            (F_s = prod F_j, S_s = sum S_j); a passing sub-group validates its jobs;
+  //   level 2: every job of a failing sub-group is checked on its own.
+  // Per-job answers are the reference's (valid iff every set of the job verifies); with few invalid jobs the
+  // final exponentiations drop from one per job to about one per kFbSub jobs.
   if (!retry.empty()) {
+    constexpr uint32_t kFbSub = 16;
     const uint32_t nr = (uint32_t)retry.size();
-    std::vector<uint32_t> rfirst{0}, ritems, rr(2 * (size_t)nr), rf(2 * (size_t)nr), rsl, rrs{0};
+    std::vector<uint32_t> rfirst{0}, ritems, rr(2 * (size_t)nr), rf(2 * (size_t)nr), rsl, rrs{0}, rset;
     for (uint32_t q = 0; q < nr; q++) {
       const auto js = job_sets(retry[q]);
       rr[2 * q] = js.first;
       rr[2 * q + 1] = js.second;
       add_slices(rsl, rrs, js.first, js.second);
+      for (uint32_t i = js.first; i < js.second; i++) rset.push_back(i);
       const auto cr = add_chunks(rfirst, ritems, js.first, js.second, mk);
       rf[2 * q] = cr.first;
       rf[2 * q + 1] = cr.second;
     }
+    const bool small_jobs = rset.size() < (size_t)32 * nr;  // per-set scalings instead of per-job MSMs
+    const uint32_t nsub = nr >= 2 * kFbSub ? (nr + kFbSub - 1) / kFbSub : 0;
+    std::vector<uint32_t> subr(2 * (size_t)nsub);
+    for (uint32_t t = 0; t < nsub; t++) {
+      subr[2 * t] = t * kFbSub;
+      subr[2 * t + 1] = std::min(nr, (t + 1) * kFbSub);
+    }
     const uint32_t nc = (uint32_t)rfirst.size() - 1;
     const uint32_t nrs = (uint32_t)(rsl.size() / 2);
-    const size_t o_rsl = 4 * (size_t)nr + rfirst.size() + ritems.size(), o_rrs = o_rsl + rsl.size();
-    const size_t words = o_rrs + rrs.size();
+    const size_t o_rsl = 4 * (size_t)nr + rfirst.size() + ritems.size(), o_rrs = o_rsl + rsl.size(),
+                 o_rset = o_rrs + rrs.size(), o_sub = o_rset + rset.size(), o_sel = o_sub + subr.size();
+    const size_t words = o_sel + nr;
     sl.h_list.ensure(words);
     sl.d_list.ensure(words);
     uint32_t* hl = sl.h_list.p;
@@ -660,25 +678,60 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     memcpy(hl + 4 * (size_t)nr + rfirst.size(), ritems.data(), ritems.size() * 4);
     memcpy(hl + o_rsl, rsl.data(), rsl.size() * 4);
     memcpy(hl + o_rrs, rrs.data(), rrs.size() * 4);
-    sl.d_msmB.ensure((size_t)MSM_BUCKET_WORDS * std::max<uint32_t>(nrs, 1));
-    sl.d_msmW.ensure((size_t)MSM_WINDOW_WORDS * nr);
-    sl.d_ok.ensure(nr);
-    sl.h_ok.ensure(nr);
-    sl.d_S.ensure((size_t)W_G2J * nr);
-    sl.d_F.ensure((size_t)W_FP12 * nr);
-    HIPCHK(hipMemcpyAsync(sl.d_list.p, hl, words * 4, hipMemcpyHostToDevice, s));
+    memcpy(hl + o_rset, rset.data(), rset.size() * 4);
+    if (nsub) memcpy(hl + o_sub, subr.data(), subr.size() * 4);
+    sl.d_ok.ensure(nr + nsub);
+    sl.h_ok.ensure(nr + nsub);
+    sl.d_S.ensure((size_t)W_G2J * (nr + nsub));
+    sl.d_F.ensure((size_t)W_FP12 * (nr + nsub));
+    uint32_t* const dS = sl.d_S.p;  // per-job S_j, F_j (stride nr), then the sub-groups' (stride nsub)
+    uint32_t* const dF = sl.d_F.p;
+    uint32_t* const dS_sub = sl.d_S.p + (size_t)W_G2J * nr;
+    uint32_t* const dF_sub = sl.d_F.p + (size_t)W_FP12 * nr;
+    HIPCHK(hipMemcpyAsync(sl.d_list.p, hl, o_sel * 4, hipMemcpyHostToDevice, s));
     PipelineBuffers pr = pb;
     pr.n_chunks = nc;
     pr.chunk_first = sl.d_list.p + 4 * (size_t)nr;
     pr.chunk_items = sl.d_list.p + 4 * (size_t)nr + rfirst.size();
     launch_miller_acc(pr, false, s);
-    launch_sig_msm(pr, sl.d_list.p + o_rsl, nrs, sl.d_list.p + o_rrs, nr, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s);
-    launch_group_reduce(pr, nullptr, sl.d_list.p + 2 * (size_t)nr, nr, sl.d_S.p, sl.d_F.p, s);
-    launch_group_check(sl.d_S.p, sl.d_F.p, nr, sl.d_ok.p, s);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, nr, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    for (uint32_t q = 0; q < nr; q++) jr[retry[q]] = sl.h_ok.p[q] ? 1 : 0;
+    if (small_jobs) {
+      // r_i sig_i for the retried sets (G2 window tables and results in the fallback's own buffers)
+      sl.d_fb.ensure((size_t)stride * 9 * W_G2J);
+      pr.rsig = sl.d_fb.p;
+      pr.scal_tab = sl.d_fb.p + (size_t)stride * W_G2J;
+      launch_sig_scale(pr, (uint32_t)rset.size(), s, sl.d_list.p + o_rset);
+      launch_group_reduce(pr, sl.d_list.p, sl.d_list.p + 2 * (size_t)nr, nr, dS, dF, s);
+    } else {
+      sl.d_msmB.ensure((size_t)MSM_BUCKET_WORDS * std::max<uint32_t>(nrs, 1));
+      sl.d_msmW.ensure((size_t)MSM_WINDOW_WORDS * nr);
+      launch_sig_msm(pr, sl.d_list.p + o_rsl, nrs, sl.d_list.p + o_rrs, nr, sl.d_msmB.p, sl.d_msmW.p, dS, s);
+      launch_group_reduce(pr, nullptr, sl.d_list.p + 2 * (size_t)nr, nr, dS, dF, s);
+    }
+    std::vector<uint32_t> sel;  // jobs to check on their own
+    if (nsub) {
+      launch_range_combine(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, s);
+      launch_group_check(dS_sub, dF_sub, nsub, sl.d_ok.p + nr, s);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(sl.h_ok.p + nr, sl.d_ok.p + nr, nsub, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      for (uint32_t t = 0; t < nsub; t++)
+        for (uint32_t q = subr[2 * t]; q < subr[2 * t + 1]; q++) {
+          if (sl.h_ok.p[nr + t]) jr[retry[q]] = 1;
+          else sel.push_back(q);
+        }
+    } else {
+      for (uint32_t q = 0; q < nr; q++) sel.push_back(q);
+    }
+    if (!sel.empty()) {
+      const uint32_t ns = (uint32_t)sel.size();
+      memcpy(hl + o_sel, sel.data(), (size_t)ns * 4);
+      HIPCHK(hipMemcpyAsync(sl.d_list.p + o_sel, hl + o_sel, (size_t)ns * 4, hipMemcpyHostToDevice, s));
+      launch_group_check(dS, dF, nr, sl.d_ok.p, s, sl.d_list.p + o_sel, ns);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, ns, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      for (uint32_t k = 0; k < ns; k++) jr[retry[sel[k]]] = sl.h_ok.p[k] ? 1 : 0;
+    }
   }
   for (uint32_t j = 0; j < nj; j++) job_result[sh.job_begin + j] = (int8_t)jr[j];
   return BLSGPU_OK;

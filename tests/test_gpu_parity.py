@@ -330,3 +330,35 @@ def test_two_shards_match_one():
         c2.close()
     want, _ = cpu.verify_jobs(threads=THREADS, **batch)
     assert np.array_equal(got, want)
+
+
+def test_msm_exceptional_buckets_vs_oracle(ctx):
+    """The bucket MSM (k_msm.hip) on inputs that hit its exceptional additions: one valid set repeated 600 times
+    (every bucket adds the same point: doublings), sets whose signatures are each other's negation, groups of
+    several MSM slices (> 256 sets), and a wrong signature among repeats (the fallback's per-job MSMs)."""
+    sks = interop_sks(4, first=5000)
+    pks = cpu.sk_to_pk(sks, threads=THREADS)
+    m = [msg(j, b"msm") for j in range(4)]
+    sig = cpu.sign(sks, b"".join(m), threads=THREADS)
+    reps = 600
+    idx = [0] * reps + [1, 2, 3]
+    sigs = [sig[96 * i: 96 * i + 96] for i in idx]
+    neg = bytes([sig[96] ^ 0x20]) + sig[97:192]  # the y-sign flag: -sig_1
+    sigs += [neg]  # -sig_1 over m_1: false, and cancels sig_1 inside buckets
+    idx += [1]
+    sigs[300] = sig[96 * 2: 96 * 3]  # set 300 carries set 2's signature: false
+    n = len(idx)
+    batch = dict(job_first_set=np.arange(n + 1), sigs=b"".join(sigs), sig_len=[96] * n,
+                 msgs=b"".join(m[i] for i in idx), pk_bytes=b"".join(pks[96 * i: 96 * i + 96] for i in idx),
+                 job_flags=np.ones(n))
+    got, st = compare(ctx, **batch)
+    want = np.ones(n, np.int8)
+    want[300] = 0
+    want[n - 1] = 0
+    assert np.array_equal(got, want) and st.batch_retries >= 1
+    # all valid: one group of 603 sets (three MSM slices), no fallback
+    ok = dict(batch, sigs=b"".join(sig[96 * i: 96 * i + 96] for i in idx[:-1]), sig_len=[96] * (n - 1),
+              job_first_set=np.arange(n), msgs=b"".join(m[i] for i in idx[:-1]),
+              pk_bytes=b"".join(pks[96 * i: 96 * i + 96] for i in idx[:-1]), job_flags=np.ones(n - 1))
+    got, st = ctx.verify_raw(**ok)
+    assert (got == 1).all() and st.batch_retries == 0
