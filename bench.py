@@ -8,7 +8,7 @@ sk_i = LE(sha256(LE32_32(i))) mod r (reference state-transition/src/util/interop
 device-resident table.  Inputs are generated on the GPU before timing (signing kernels) and are resident
 in host pinned staging; one step = one blsgpu_verify call = H2D + full verification + per-job results.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1|C2|C3|C4|C5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
 
 Prints one JSON line (rank 0).  Multi-GPU: each rank verifies its own 16,384 sets (weak scaling, no
@@ -71,8 +71,8 @@ def message_variant(ctx, w, v):
 def build_workload(ctx, config, rank, world=1, n_dev=1):
     """Returns dict of numpy inputs for verify_raw + description.  n_dev > 1: one call spans n_dev in-process
     devices (the runtime shards it), so C2 carries 16,384 sets per device."""
-    if config == "C2":
-        n = 16384 * n_dev
+    if config in ("C1", "C2"):
+        n = (128 if config == "C1" else 16384) * n_dev
         sks, pks = gen_keys(ctx, n)
         ctx.upload_pubkeys(0, pks)
         mkeys = [rank * n + j for j in range(n)]
@@ -83,7 +83,9 @@ def build_workload(ctx, config, rank, world=1, n_dev=1):
                  sig_len=np.full(n, 96, np.uint32), msgs=np.frombuffer(b"".join(msgs), np.uint8),
                  set_pk_first=np.arange(n + 1, dtype=np.uint32), pk_index=np.arange(n, dtype=np.uint32),
                  job_flags=np.ones(n, np.uint8), sig_stride=96, pks_table=pks)
-        desc = {"workload": "C2 gossip attestation flood: 16384 single-pubkey sets per GPU, 1 set per batchable job",
+        desc = {"workload": ("C1 reference perf bench shape: 128 random single-pubkey sets per call, 1 set per batchable job"
+                             if config == "C1" else
+                             "C2 gossip attestation flood: 16384 single-pubkey sets per GPU, 1 set per batchable job"),
                 "sets_per_step_per_gpu": n // n_dev, "pubkeys_per_set": 1, "pk_mode": "device table",
                 "sig_encoding": "compressed 96 B", "distinct_messages": n}
         return w, n, desc, 1
@@ -365,7 +367,7 @@ def main():
     ap.add_argument("--group-sets", type=int, default=1024)
     ap.add_argument("--inflight", type=int, default=32,
                     help="verifySignatureSets calls in flight per GPU (runtime slots); 1 = strictly serial")
-    ap.add_argument("--slots", type=int, default=4,
+    ap.add_argument("--slots", type=int, default=2,
                     help="runtime slots per GPU (0 = one per in-flight call); fewer slots than calls in flight make "
                          "each slot merge the queued calls into one pipeline run")
     ap.add_argument("--merge-sets", type=int, default=131072, help="max sets of one merged pipeline run (0 = never)")
@@ -397,7 +399,7 @@ def main():
     # one process per GPU under torch.distributed.run; without a launcher, --gpus N uses N devices in-process
     # (each call sharded over them by the runtime)
     n_dev = args.gpus if world == 1 else 1
-    if n_dev > 1 and args.config != "C2":
+    if n_dev > 1 and args.config not in ("C1", "C2"):
         raise SystemExit("in-process multi-GPU runs take --config C2 (launch other configs per rank)")
     devices = list(range(n_dev)) if world == 1 else [local_rank]
     ctx = Context(devices)

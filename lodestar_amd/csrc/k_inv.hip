@@ -94,8 +94,9 @@ void launch_batch_inv(const uint32_t* src, uint32_t src_stride, int w0, uint32_t
 }
 void launch_pk_affine(const PipelineBuffers& b, uint32_t n, hipStream_t s) {
   if (!n) return;
-  launch_batch_inv(b.pk_jac, b.n, 2 * W_FP, b.inv_buf, n, s);
-  hipLaunchKernelGGL(k_pk_affine, grid_for(n), dim3(WAVE), 0, s, b, n, b.inv_buf, b.status + b.n);
+  uint32_t* inv = b.inv_buf_pk ? b.inv_buf_pk : b.inv_buf;
+  launch_batch_inv(b.pk_jac, b.n, 2 * W_FP, inv, n, s);
+  hipLaunchKernelGGL(k_pk_affine, grid_for(n), dim3(WAVE), 0, s, b, n, inv, b.status + b.n);
 }
 void launch_h_affine(const PipelineBuffers& b, hipStream_t s) {
   if (!b.n_umsg) return;

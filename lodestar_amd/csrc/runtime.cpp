@@ -94,8 +94,11 @@ inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // One in-flight shard on one device: a stream and every per-call buffer.
 struct Slot {
-  hipStream_t stream = nullptr;
-  hipEvent_t ev[kStages + 1] = {};
+  // Three streams per slot: the run's independent branches overlap -- signatures + the batch tail on `stream`,
+  // hash_to_G2 + Miller lines on `stream_msg`, pubkey aggregation + r_i pk_i on `stream_pk` -- joined by events.
+  hipStream_t stream = nullptr, stream_msg = nullptr, stream_pk = nullptr;
+  hipEvent_t join_in = nullptr, join_msg = nullptr, join_pk = nullptr;  // no timing
+  hipEvent_t ev[2 * (kStages + 1)] = {};  // profile: (start, end) per stage; pair kStages = the Miller lines
   // d_in / h_in: every per-call input packed into one arena (one H2D transfer); d_res / h_res: job errors +
   // group verdicts (one D2H transfer).
   DevBuf<uint8_t> d_in, d_res, d_bytes, d_ok;
@@ -501,7 +504,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   sl.d_msmW.ensure((size_t)MSM_WINDOW_WORDS * max_ranges);
   // work area: per set sig_aff, pk_jac, pk_aff, f_chunk, the G1 window table of r_i pk_i, inv_buf (+ per unit
   // unit_p), per message h_aff, h_jac, h_norm, h_prep
-  const size_t per_set = W_G2A + W_G1J + W_G1A + W_FP12 + 8 * W_G1J + W_FP + (merged ? W_G1A : 0);
+  const size_t per_set = W_G2A + W_G1J + W_G1A + W_FP12 + 8 * W_G1J + 2 * W_FP + (merged ? W_G1A : 0);
   sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * (W_G2A + W_G2J + W_FP + 14 * W_FP));
   sl.d_lines.ensure((size_t)nm * kMillerLineWords);
   hipStream_t s = sl.stream;
@@ -548,6 +551,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.chunk_first = reinterpret_cast<uint32_t*>(din + o_cfirst);
   pb.chunk_items = reinterpret_cast<uint32_t*>(din + o_citems);
   pb.inv_buf = w; w += (size_t)stride * W_FP;  // n_umsg <= n
+  pb.inv_buf_pk = w; w += (size_t)stride * W_FP;  // the pubkey branch's own (it runs beside the hash branch)
   pb.h_aff = w; w += (size_t)nm * W_G2A;
   pb.h_jac = w; w += (size_t)nm * W_G2J;
   pb.h_norm = w; w += (size_t)nm * W_FP;
@@ -562,37 +566,62 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.job_err = reinterpret_cast<int8_t*>(sl.d_res.p);
 
   // ---- kernel pipeline ------------------------------------------------------------------------------------
+  // DAG of one run: signatures (decode) | messages (hash_to_G2 -> affine -> Miller lines) | pubkeys (aggregate ->
+  // r_i pk_i -> affine) run on three streams after the input copy; the job mask waits for the pubkey branch,
+  // the Miller accumulation for the message branch.  An isolated call's critical path drops from the sum of
+  // the stages to hash + lines + accumulation + tail; a full chip just interleaves the branches.
   const bool prof = opt.profile;
-  auto mark = [&](int k) {
-    if (prof) HIPCHK(hipEventRecord(sl.ev[k], s));
+  hipStream_t sm = sl.stream_msg, sp = sl.stream_pk;
+  auto beg = [&](int k, hipStream_t st) {
+    if (prof) HIPCHK(hipEventRecord(sl.ev[2 * k], st));
   };
-  mark(0);
+  auto end = [&](int k, hipStream_t st) {
+    if (prof) HIPCHK(hipEventRecord(sl.ev[2 * k + 1], st));
+  };
+  HIPCHK(hipEventRecord(sl.join_in, s));
+  HIPCHK(hipStreamWaitEvent(sm, sl.join_in, 0));
+  HIPCHK(hipStreamWaitEvent(sp, sl.join_in, 0));
+  // messages
+  beg(1, sm);
+  launch_hash_to_g2(pb, sm);
+  launch_h_affine(pb, sm);
+  end(1, sm);
+  beg(kStages, sm);
+  launch_miller_lines(pb, sm);
+  end(kStages, sm);
+  HIPCHK(hipEventRecord(sl.join_msg, sm));
+  // pubkeys
+  beg(2, sp);
+  if ((table_mode || bytes_agg) && pb.n_agg) launch_pk_aggregate(pb, n, sp);
+  end(2, sp);
+  beg(3, sp);
+  launch_pk_finish(pb, n, sp);
+  launch_pk_affine(pb, n, sp);
+  end(3, sp);
+  HIPCHK(hipEventRecord(sl.join_pk, sp));
+  // signatures, then the batch equation
+  beg(0, s);
   launch_sig_decode(pb, n, s);
-  mark(1);
-  launch_hash_to_g2(pb, s);
-  launch_h_affine(pb, s);
-  mark(2);
-  if ((table_mode || bytes_agg) && pb.n_agg) launch_pk_aggregate(pb, n, s);
-  mark(3);
-  launch_pk_finish(pb, n, s);
-  launch_pk_affine(pb, n, s);
-  mark(4);
+  end(0, s);
+  HIPCHK(hipStreamWaitEvent(s, sl.join_pk, 0));
+  beg(4, s);
   launch_job_mask(pb, s);
   const uint32_t* d_slices = reinterpret_cast<uint32_t*>(din + o_slices);
   const uint32_t* d_rslices = reinterpret_cast<uint32_t*>(din + o_rslices);
   launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s);
-  mark(5);
-  launch_miller_lines(pb, s);
+  end(4, s);
+  HIPCHK(hipStreamWaitEvent(s, sl.join_msg, 0));
+  beg(5, s);
   if (merged) launch_unit_aggregate(pb, s);
   launch_miller_acc(pb, merged, s);
-  mark(6);
-  const uint32_t* d_ranges = reinterpret_cast<uint32_t*>(din + o_ranges);
+  end(5, s);
   const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
-  (void)d_ranges;
+  beg(6, s);
   launch_group_reduce(pb, nullptr, d_franges, ng0, sl.d_S.p, sl.d_F.p, s);
-  mark(7);
+  end(6, s);
+  beg(7, s);
   launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, s);
-  mark(8);
+  end(7, s);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(sl.h_res.p, sl.d_res.p, o_ok + ng0, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -604,7 +633,12 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   if (prof) {
     for (int k = 0; k < kStages; k++) {
       float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, sl.ev[k], sl.ev[k + 1]));
+      HIPCHK(hipEventElapsedTime(&ms, sl.ev[2 * k], sl.ev[2 * k + 1]));
+      if (k == 5) {  // the Miller stage = lines (message branch) + accumulation
+        float ml = 0;
+        HIPCHK(hipEventElapsedTime(&ml, sl.ev[2 * kStages], sl.ev[2 * kStages + 1]));
+        ms += ml;
+      }
       st.stage_ms[k] += ms;
     }
   }
@@ -985,6 +1019,9 @@ void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet sh
   Slot* s = new Slot();
   HIPCHK(hipSetDevice(d->id));
   HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&s->stream_msg, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&s->stream_pk, hipStreamNonBlocking));
+  for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk}) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
   d->slots.push_back(s);
   d->workers.emplace_back(worker_loop, d, s);
@@ -999,11 +1036,15 @@ void destroy_device(Device* d) {
   for (auto& t : d->workers) t.join();
   (void)hipSetDevice(d->id);
   for (Slot* s : d->slots) {
-    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    for (hipStream_t st : {s->stream, s->stream_msg, s->stream_pk})
+      if (st) (void)hipStreamSynchronize(st);
     s->release_all();
     for (auto& e : s->ev)
       if (e) (void)hipEventDestroy(e);
-    if (s->stream) (void)hipStreamDestroy(s->stream);
+    for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk})
+      if (e) (void)hipEventDestroy(e);
+    for (hipStream_t st : {s->stream, s->stream_msg, s->stream_pk})
+      if (st) (void)hipStreamDestroy(st);
     delete s;
   }
   d->helper.release_all();
