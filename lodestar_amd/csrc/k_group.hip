@@ -68,17 +68,17 @@ __global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const 
 
 // One 128-lane workgroup per group: the Miller loop and the final exponentiation run as cooperative Fp12
 // arithmetic (gt_wave.hpp), one Fp product per lane per step.
-__global__ __launch_bounds__(GTW_LANES) void k_group_check(const uint32_t* S_in, const uint32_t* F_in, uint32_t ng,
-                                                           const uint32_t* sel, uint8_t* ok) {
-  __shared__ GtwLds sh;
-  const uint32_t t = threadIdx.x;
-  const uint32_t g = sel ? sel[blockIdx.x] : blockIdx.x;  // entry checked (S_in / F_in stride ng); verdict ok[blockIdx.x]
-  // F: SoA tower layout (Fp2 slots c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2) -> LDS w-basis
-  for (uint32_t w = t; w < W_FP12; w += GTW_LANES) {
-    const uint32_t slot = w / (2 * W_FP), rest = w % (2 * W_FP);
-    const uint32_t k = slot < 3 ? 2 * slot : 2 * (slot - 3) + 1;
-    sh.F[k * 2 * W_FP + rest] = F_in[(size_t)w * ng + g];
-  }
+//   G_in == nullptr: FinalExp(F * MillerLoop(-g1, S)) == 1 (the fallback's per-job / sub-group checks);
+//   G_in != nullptr: FinalExp(F * G) == 1 with G = MillerLoop(-g1, S) from k_group_sig_miller, which the batch
+//                    pass runs right after the MSM, beside the message branch (off the call's critical path).
+// F / G in HBM: SoA tower layout (Fp2 slots c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2); in LDS: the w-basis.
+__device__ __forceinline__ uint32_t gtw_lds_word(uint32_t w) {
+  const uint32_t slot = w / (2 * W_FP), rest = w % (2 * W_FP);
+  const uint32_t k = slot < 3 ? 2 * slot : 2 * (slot - 3) + 1;
+  return k * 2 * W_FP + rest;
+}
+// lane 0: S -> affine in QA; returns (through LDS) whether S is finite
+__device__ __forceinline__ void gtw_load_S(GtwLds& sh, const uint32_t* S_in, uint32_t ng, uint32_t g, uint32_t t) {
   if (t == 0) {
     g2a Sa;
     const bool fin = jac_to_aff(ld_g2j(S_in, ng, g), Sa);
@@ -90,8 +90,35 @@ __global__ __launch_bounds__(GTW_LANES) void k_group_check(const uint32_t* S_in,
     }
     sh.flag = fin ? 1u : 0u;
   }
+}
+
+__global__ __launch_bounds__(GTW_LANES) void k_group_sig_miller(const uint32_t* S_in, uint32_t ng, uint32_t* G_out) {
+  __shared__ GtwLds sh;
+  const uint32_t g = blockIdx.x, t = threadIdx.x;
+  gtw_load_S(sh, S_in, ng, g, t);
   gtw_sync();
-  if (sh.flag) {
+  if (sh.flag)
+    gtw_miller_loop(sh.G, sh.QA, G1_GEN_X, G1_NEG_GEN_Y, sh.TB, sh.L, sh.S, t);
+  else
+    gtw_set_one(sh.G, t);
+  gtw_sync();
+  for (uint32_t w = t; w < W_FP12; w += GTW_LANES) G_out[(size_t)w * ng + g] = sh.G[gtw_lds_word(w)];
+}
+
+__global__ __launch_bounds__(GTW_LANES) void k_group_check(const uint32_t* S_in, const uint32_t* F_in, uint32_t ng,
+                                                           const uint32_t* G_in, const uint32_t* sel, uint8_t* ok) {
+  __shared__ GtwLds sh;
+  const uint32_t t = threadIdx.x;
+  const uint32_t g = sel ? sel[blockIdx.x] : blockIdx.x;  // entry checked (S_in / F_in stride ng); verdict ok[blockIdx.x]
+  for (uint32_t w = t; w < W_FP12; w += GTW_LANES) {
+    sh.F[gtw_lds_word(w)] = F_in[(size_t)w * ng + g];
+    if (G_in) sh.G[gtw_lds_word(w)] = G_in[(size_t)w * ng + g];
+  }
+  if (!G_in) gtw_load_S(sh, S_in, ng, g, t);
+  gtw_sync();
+  if (G_in) {
+    gtw_mul<false>(sh.F, sh.F, sh.G, sh.S, t);
+  } else if (sh.flag) {
     gtw_miller_loop(sh.G, sh.QA, G1_GEN_X, G1_NEG_GEN_Y, sh.TB, sh.L, sh.S, t);
     gtw_mul<false>(sh.F, sh.F, sh.G, sh.S, t);
   }
@@ -143,9 +170,12 @@ void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, c
   if (ng) hipLaunchKernelGGL(k_group_reduce, dim3(ng), dim3(WAVE), 0, s, b, set_ranges, f_ranges, ng, S, F);
 }
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s,
-                        const uint32_t* sel, uint32_t n_sel) {
+                        const uint32_t* sel, uint32_t n_sel, const uint32_t* G) {
   const uint32_t n = sel ? n_sel : ng;
-  if (n) hipLaunchKernelGGL(k_group_check, dim3(n), dim3(GTW_LANES), 0, s, S, F, ng, sel, ok);
+  if (n) hipLaunchKernelGGL(k_group_check, dim3(n), dim3(GTW_LANES), 0, s, S, F, ng, G, sel, ok);
+}
+void launch_group_sig_miller(const uint32_t* S, uint32_t ng, uint32_t* G, hipStream_t s) {
+  if (ng) hipLaunchKernelGGL(k_group_sig_miller, dim3(ng), dim3(GTW_LANES), 0, s, S, ng, G);
 }
 void launch_range_combine(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,
                           uint32_t n_out, uint32_t* S_out, uint32_t* F_out, hipStream_t s) {

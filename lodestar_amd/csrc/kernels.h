@@ -116,8 +116,10 @@ void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, c
                          uint32_t n_groups, uint32_t* S, uint32_t* F, hipStream_t s);
 // check: ok_g = FinalExp(F_g * MillerLoop(-g1, S_g)) == 1
 // (sel: check only the entries sel[0 .. n_sel), verdict q -> ok[q])
+// (G: MillerLoop(-g1, S_g) precomputed by launch_group_sig_miller, W_FP12 SoA stride n_groups; null = computed here)
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t n_groups, uint8_t* ok, hipStream_t s,
-                        const uint32_t* sel = nullptr, uint32_t n_sel = 0);
+                        const uint32_t* sel = nullptr, uint32_t n_sel = 0, const uint32_t* G = nullptr);
+void launch_group_sig_miller(const uint32_t* S, uint32_t n_groups, uint32_t* G, hipStream_t s);
 // fallback sub-groups: S_out[r] = sum, F_out[r] = prod of the per-job entries ranges[2r] .. ranges[2r+1]
 void launch_range_combine(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,
                           uint32_t n_out, uint32_t* S_out, uint32_t* F_out, hipStream_t s);

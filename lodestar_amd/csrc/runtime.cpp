@@ -49,20 +49,30 @@ struct HipError {
     if (_e != hipSuccess) throw HipError{_e}; \
   } while (0)
 
+// Device buffer that only grows.  A slot's buffers grow stream-ordered (hipFreeAsync / hipMallocAsync on the
+// slot's stream): a plain hipFree waits for the whole device, so a merged run larger than any before would stall
+// every other slot's work (seen as 1.4-2.5 s call latencies in the bench's tail).  Growth doubles.
 template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t cap = 0;
+  hipStream_t st = nullptr;  // set for slot buffers
   void ensure(size_t n) {
     if (n <= cap) return;
-    if (p) HIPCHK(hipFree(p));
-    p = nullptr;
-    size_t c = std::max<size_t>(n, cap * 3 / 2);
-    HIPCHK(hipMalloc((void**)&p, c * sizeof(T)));
+    const size_t c = std::max<size_t>(n, cap * 2);
+    if (st) {
+      if (p) HIPCHK(hipFreeAsync(p, st));
+      p = nullptr;
+      HIPCHK(hipMallocAsync((void**)&p, c * sizeof(T), st));
+    } else {
+      if (p) HIPCHK(hipFree(p));
+      p = nullptr;
+      HIPCHK(hipMalloc((void**)&p, c * sizeof(T)));
+    }
     cap = c;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) (void)(st ? hipFreeAsync(p, st) : hipFree(p));
     p = nullptr;
     cap = 0;
   }
@@ -76,7 +86,7 @@ struct HostBuf {  // pinned staging
     if (n <= cap) return;
     if (p) HIPCHK(hipHostFree(p));
     p = nullptr;
-    size_t c = std::max<size_t>(n, cap * 3 / 2);
+    size_t c = std::max<size_t>(n, cap * 2);
     HIPCHK(hipHostMalloc((void**)&p, c * sizeof(T), hipHostMallocDefault));
     cap = c;
   }
@@ -98,18 +108,23 @@ struct Slot {
   // hash_to_G2 + Miller lines on `stream_msg`, pubkey aggregation + r_i pk_i on `stream_pk` -- joined by events.
   hipStream_t stream = nullptr, stream_msg = nullptr, stream_pk = nullptr;
   hipEvent_t join_in = nullptr, join_msg = nullptr, join_pk = nullptr;  // no timing
-  hipEvent_t ev[2 * (kStages + 1)] = {};  // profile: (start, end) per stage; pair kStages = the Miller lines
+  hipEvent_t ev[2 * (kStages + 2)] = {};  // profile: (start, end) per stage; pairs kStages, kStages + 1 = the
+                                          // Miller lines, the groups' MillerLoop(-g1, S) (parts of stages 5, 7)
   // d_in / h_in: every per-call input packed into one arena (one H2D transfer); d_res / h_res: job errors +
   // group verdicts (one D2H transfer).
   DevBuf<uint8_t> d_in, d_res, d_bytes, d_ok;
-  DevBuf<uint32_t> d_work, d_lines, d_S, d_F, d_list, d_msmB, d_msmW, d_fb;
+  DevBuf<uint32_t> d_work, d_lines, d_S, d_F, d_G, d_list, d_msmB, d_msmW, d_fb;
   HostBuf<uint8_t> h_in, h_res, h_ok;
   HostBuf<uint32_t> h_list;
 
+  void set_stream(hipStream_t st) {
+    for (auto* b : {&d_in, &d_res, &d_bytes, &d_ok}) b->st = st;
+    for (auto* b : {&d_work, &d_lines, &d_S, &d_F, &d_G, &d_list, &d_msmB, &d_msmW, &d_fb}) b->st = st;
+  }
   void release_all() {
     d_in.release(); d_res.release(); d_bytes.release(); d_ok.release();
     d_work.release(); d_lines.release(); d_S.release(); d_F.release(); d_list.release();
-    d_msmB.release(); d_msmW.release(); d_fb.release();
+    d_msmB.release(); d_msmW.release(); d_fb.release(); d_G.release();
     h_in.release(); h_res.release(); h_ok.release(); h_list.release();
   }
 };
@@ -500,6 +515,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   sl.h_res.ensure(res_bytes);
   sl.d_S.ensure((size_t)W_G2J * max_ranges);
   sl.d_F.ensure((size_t)W_FP12 * max_ranges);
+  sl.d_G.ensure((size_t)W_FP12 * std::max<uint32_t>(ng0, 1));
   sl.d_msmB.ensure((size_t)MSM_BUCKET_WORDS * std::max<uint32_t>(n_slices, 1));
   sl.d_msmW.ensure((size_t)MSM_WINDOW_WORDS * max_ranges);
   // work area: per set sig_aff, pk_jac, pk_aff, f_chunk, the G1 window table of r_i pk_i, inv_buf (+ per unit
@@ -610,6 +626,10 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   const uint32_t* d_rslices = reinterpret_cast<uint32_t*>(din + o_rslices);
   launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s);
   end(4, s);
+  // MillerLoop(-g1, S_g) of every group now, while the message branch still runs
+  beg(kStages + 1, s);
+  launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, s);
+  end(kStages + 1, s);
   HIPCHK(hipStreamWaitEvent(s, sl.join_msg, 0));
   beg(5, s);
   if (merged) launch_unit_aggregate(pb, s);
@@ -620,7 +640,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   launch_group_reduce(pb, nullptr, d_franges, ng0, sl.d_S.p, sl.d_F.p, s);
   end(6, s);
   beg(7, s);
-  launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, s);
+  launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, s, nullptr, 0, sl.d_G.p);
   end(7, s);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(sl.h_res.p, sl.d_res.p, o_ok + ng0, hipMemcpyDeviceToHost, s));
@@ -634,9 +654,10 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     for (int k = 0; k < kStages; k++) {
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, sl.ev[2 * k], sl.ev[2 * k + 1]));
-      if (k == 5) {  // the Miller stage = lines (message branch) + accumulation
+      if (k == 5 || k == 7) {  // Miller stage = lines + accumulation; group check = MillerLoop(-g1, S) + final exp.
+        const int x = k == 5 ? kStages : kStages + 1;
         float ml = 0;
-        HIPCHK(hipEventElapsedTime(&ml, sl.ev[2 * kStages], sl.ev[2 * kStages + 1]));
+        HIPCHK(hipEventElapsedTime(&ml, sl.ev[2 * x], sl.ev[2 * x + 1]));
         ms += ml;
       }
       st.stage_ms[k] += ms;
@@ -1021,6 +1042,7 @@ void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet sh
   HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&s->stream_msg, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&s->stream_pk, hipStreamNonBlocking));
+  s->set_stream(s->stream);
   for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk}) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
   d->slots.push_back(s);
@@ -1039,6 +1061,7 @@ void destroy_device(Device* d) {
     for (hipStream_t st : {s->stream, s->stream_msg, s->stream_pk})
       if (st) (void)hipStreamSynchronize(st);
     s->release_all();
+    if (s->stream) (void)hipStreamSynchronize(s->stream);  // the stream-ordered frees
     for (auto& e : s->ev)
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk})
