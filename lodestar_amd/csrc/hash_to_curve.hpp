@@ -249,6 +249,19 @@ BLS_HDNI void hash_to_g2_prep(const uint8_t msg[32], h2c_prep& h) {
   const fp2 a1 = fp2_select(fp2_is_zero(h.tv1), fp2_one(), h.tv1);
   h.d = fp2_mul(a0, a1);
 }
+// One of the two maps (j = 0, 1) of the finish step: iso3(SSWU(u_j)) as a Jacobian point.  The pipeline runs the
+// two maps of a message on two lanes (k_hash_map), then sums and clears the cofactor (k_hash_clear).
+BLS_HDNI g2j hash_to_g2_map_j(const h2c_prep& h, const fp2& dinv, int j) {
+  const bool z0 = fp2_is_zero(h.tv0), z1 = fp2_is_zero(h.tv1);
+  const fp2 a_other = j == 0 ? fp2_select(z1, fp2_one(), h.tv1) : fp2_select(z0, fp2_one(), h.tv0);
+  const bool zj = j == 0 ? z0 : z1;
+  const fp2 inv = fp2_select(zj, fp2_zero(), fp2_mul(dinv, a_other));
+  // select the operands, then ONE call: lanes j = 0 and 1 of a wave run the same instruction stream
+  const bool j0 = j == 0;
+  const g2a q = sswu_map(fp2_select(j0, h.u0, h.u1), fp2_select(j0, h.Zu2_0, h.Zu2_1), fp2_select(j0, h.tv0, h.tv1), inv);
+  return iso3_map_jac(q);
+}
+
 BLS_HDNI g2j hash_to_g2_finish(const h2c_prep& h, const fp2& dinv) {
   const bool z0 = fp2_is_zero(h.tv0), z1 = fp2_is_zero(h.tv1);
   const fp2 a0 = fp2_select(z0, fp2_one(), h.tv0);

@@ -2,8 +2,8 @@
 // attestations of one committee share AttestationData, reference chain/validation/attestation.ts:131-138).
 // Two kernels around the maps' one field inversion, which is batched over the messages in between
 // (k_inv.hip, Montgomery's simultaneous inversion): k_hash_prep (hash_to_field .. d = a0 a1, stored with
-// N(d)) -> k_batch_inv(N(d)) -> k_hash_map (SSWU x2, isogeny, cofactor clearing; Jacobian H(m) + N(z)) ->
-// k_batch_inv(N(z)) -> k_h_affine.
+// N(d)) -> k_batch_inv(N(d)) -> k_hash_map (one SSWU map + isogeny per lane, two lanes per message) ->
+// k_hash_clear (sum, cofactor clearing; Jacobian H(m) + N(z)) -> k_batch_inv(N(z)) -> k_h_affine.
 #include "k_common.hpp"
 
 #define W_HPREP (7 * 2 * W_FP)
@@ -44,14 +44,25 @@ STAGE_KERNEL void k_hash_prep(PipelineBuffers b) {
   st_fp(b.h_norm, b.nm, u, 0, fp2_norm(h.d));
 }
 
-// inv: 1 / N(d) from the batch inversion; d^-1 = conj(d) / N(d).  Jacobian out (affine conversion batched).
+// inv: 1 / N(d) from the batch inversion; d^-1 = conj(d) / N(d).  Two lanes per message (lane pair (u, j)): each
+// runs one SSWU map + isogeny -> h_q[j] (the two maps of a message are independent, so a small call's hash
+// latency drops by one map).
 STAGE_KERNEL_W(BLSGPU_WPE_HASH) void k_hash_map(PipelineBuffers b, const uint32_t* inv) {
-  uint32_t u = blockIdx.x * WAVE + threadIdx.x;
-  if (u >= b.n_umsg) return;
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  if (q >= 2 * b.n_umsg) return;
+  const uint32_t u = q >> 1, j = q & 1;
   const h2c_prep h = ld_prep(b.h_prep, b.nm, u);
   const fp ni = ld_fp(inv, b.n_umsg, u, 0);
   const fp2 dinv = fp2_make(fp_mul(h.d.c0, ni), fp_neg(fp_mul(h.d.c1, ni)));
-  const g2j H = hash_to_g2_finish(h, dinv);
+  st_g2j(b.h_q, 2 * b.nm, q, hash_to_g2_map_j(h, dinv, (int)j));
+}
+
+// Q = q0 + q1, cofactor clearing (RFC 9380 G.3); Jacobian out + N(z) for the batched affine conversion.
+STAGE_KERNEL_W(BLSGPU_WPE_HASH) void k_hash_clear(PipelineBuffers b) {
+  const uint32_t u = blockIdx.x * WAVE + threadIdx.x;
+  if (u >= b.n_umsg) return;
+  const g2j Q = jac_add(ld_g2j(b.h_q, 2 * b.nm, 2 * u), ld_g2j(b.h_q, 2 * b.nm, 2 * u + 1));
+  const g2j H = clear_cofactor_g2(Q);
   st_g2j(b.h_jac, b.nm, u, H);
   st_fp(b.h_norm, b.nm, u, 0, fp2_norm(H.z));
 }
@@ -62,5 +73,6 @@ void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s) {
   if (!b.n_umsg) return;
   hipLaunchKernelGGL(k_hash_prep, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
   launch_batch_inv(b.h_norm, b.nm, 0, b.inv_buf, b.n_umsg, s);
-  hipLaunchKernelGGL(k_hash_map, grid_for(b.n_umsg), dim3(WAVE), 0, s, b, b.inv_buf);
+  hipLaunchKernelGGL(k_hash_map, grid_for(2 * b.n_umsg), dim3(WAVE), 0, s, b, b.inv_buf);
+  hipLaunchKernelGGL(k_hash_clear, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
 }

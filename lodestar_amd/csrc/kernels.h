@@ -60,6 +60,7 @@ struct PipelineBuffers {
   uint32_t* h_jac;    // W_G2J, per message: H(m) before the batched affine conversion (k_inv.hip)
   uint32_t* h_norm;   // W_FP, per message: N(d) of the hash prep, then N(z) of h_jac
   uint32_t* h_prep;   // 7 x W_FP2, per message: the hash_to_G2 state across its batched inversion (k_hash.hip)
+  uint32_t* h_q;      // 2 x W_G2J, per message: the two mapped points iso3(SSWU(u_j)) (stride 2 nm, k_hash.hip)
   uint32_t* inv_buf;     // W_FP, per max(set, message): batch inversion output of the message branch (k_inv.hip)
   uint32_t* inv_buf_pk;  // W_FP, per set: the pubkey branch's (the two branches run on different streams)
   uint32_t* pk_jac;   // W_G1J, per set (aggregate)

@@ -521,7 +521,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // work area: per set sig_aff, pk_jac, pk_aff, f_chunk, the G1 window table of r_i pk_i, inv_buf (+ per unit
   // unit_p), per message h_aff, h_jac, h_norm, h_prep
   const size_t per_set = W_G2A + W_G1J + W_G1A + W_FP12 + 8 * W_G1J + 2 * W_FP + (merged ? W_G1A : 0);
-  sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * (W_G2A + W_G2J + W_FP + 14 * W_FP));
+  sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * (W_G2A + W_G2J + W_FP + 14 * W_FP + 2 * W_G2J));
   sl.d_lines.ensure((size_t)nm * kMillerLineWords);
   hipStream_t s = sl.stream;
   uint8_t* const din = sl.d_in.p;
@@ -571,7 +571,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.h_aff = w; w += (size_t)nm * W_G2A;
   pb.h_jac = w; w += (size_t)nm * W_G2J;
   pb.h_norm = w; w += (size_t)nm * W_FP;
-  pb.h_prep = w;
+  pb.h_prep = w; w += (size_t)nm * 14 * W_FP;
+  pb.h_q = w;
   pb.lines = sl.d_lines.p;
   uint8_t* const db = sl.d_bytes.p;
   pb.flags = db + ob_flags;
