@@ -160,7 +160,49 @@ __global__ __launch_bounds__(WAVE) void k_range_combine(const uint32_t* S_in, co
   }
 }
 
+// ---- lane-per-item forms of the fallback's reductions (many tiny ranges: one lane each) ----------------------
+
+// lane per range: S = sum of the range's included r_i sig_i (b.rsig), F = prod of its Miller chunks (b.f_chunk)
+STAGE_KERNEL void k_group_reduce_lane(PipelineBuffers b, const uint32_t* set_ranges, const uint32_t* f_ranges,
+                                      uint32_t ng, uint32_t* S_out, uint32_t* F_out) {
+  const uint32_t g = blockIdx.x * WAVE + threadIdx.x;
+  if (g >= ng) return;
+  g2j S = jac_infinity<fp2>();
+  for (uint32_t i = set_ranges[2 * g]; i < set_ranges[2 * g + 1]; i++)
+    if (b.include[i]) S = jac_add(S, ld_g2j(b.rsig, b.n, i));
+  fp12 F = fp12_one();
+  for (uint32_t c = f_ranges[2 * g]; c < f_ranges[2 * g + 1]; c++) F = fp12_mul(F, ld_fp12(b.f_chunk, b.n, c));
+  st_g2j(S_out, ng, g, S);
+  st_fp12(F_out, ng, g, F);
+}
+
+// lane per sub-group: S_out[r] = sum, F_out[r] = prod of entries ranges[2r] .. ranges[2r+1] (stride n_in)
+STAGE_KERNEL void k_range_combine_lane(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,
+                                       uint32_t n_out, uint32_t* S_out, uint32_t* F_out) {
+  const uint32_t r = blockIdx.x * WAVE + threadIdx.x;
+  if (r >= n_out) return;
+  g2j S = jac_infinity<fp2>();
+  fp12 F = fp12_one();
+  for (uint32_t e = ranges[2 * r]; e < ranges[2 * r + 1]; e++) {
+    S = jac_add(S, ld_g2j(S_in, n_in, e));
+    F = fp12_mul(F, ld_fp12(F_in, n_in, e));
+  }
+  st_g2j(S_out, n_out, r, S);
+  st_fp12(F_out, n_out, r, F);
+}
+
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
+
+void launch_group_reduce_lane(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
+                              uint32_t ng, uint32_t* S, uint32_t* F, hipStream_t s) {
+  if (ng) hipLaunchKernelGGL(k_group_reduce_lane, grid_for(ng), dim3(WAVE), 0, s, b, set_ranges, f_ranges, ng, S, F);
+}
+void launch_range_combine_lane(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,
+                               uint32_t n_out, uint32_t* S_out, uint32_t* F_out, hipStream_t s) {
+  if (n_out)
+    hipLaunchKernelGGL(k_range_combine_lane, grid_for(n_out), dim3(WAVE), 0, s, S_in, F_in, n_in, ranges, n_out, S_out,
+                       F_out);
+}
 
 void launch_job_mask(const PipelineBuffers& b, hipStream_t s) {
   if (b.n_jobs) hipLaunchKernelGGL(k_job_mask, grid_for(b.n_jobs), dim3(WAVE), 0, s, b);

@@ -121,6 +121,11 @@ void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, c
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t n_groups, uint8_t* ok, hipStream_t s,
                         const uint32_t* sel = nullptr, uint32_t n_sel = 0, const uint32_t* G = nullptr);
 void launch_group_sig_miller(const uint32_t* S, uint32_t n_groups, uint32_t* G, hipStream_t s);
+// lane-per-item forms (one lane per range / sub-group) for the fallback's many tiny ranges
+void launch_group_reduce_lane(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
+                              uint32_t n_groups, uint32_t* S, uint32_t* F, hipStream_t s);
+void launch_range_combine_lane(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,
+                               uint32_t n_out, uint32_t* S_out, uint32_t* F_out, hipStream_t s);
 // fallback sub-groups: S_out[r] = sum, F_out[r] = prod of the per-job entries ranges[2r] .. ranges[2r+1]
 void launch_range_combine(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,
                           uint32_t n_out, uint32_t* S_out, uint32_t* F_out, hipStream_t s);

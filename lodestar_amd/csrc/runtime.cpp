@@ -701,6 +701,11 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // final exponentiations drop from one per job to about one per kFbSub jobs.
   if (!retry.empty()) {
     constexpr uint32_t kFbSub = 16;
+    // from this many sub-groups on, one lane per sub-group combines its 16 entries (instead of a wave per
+    // sub-group).  The checks stay one 128-lane workgroup each: a lane-per-check final exponentiation gave the
+    // same C5 throughput at 56% more latency (profiles/r02_configs_fallback.json), and its call frames need
+    // 8-12 KB/lane of scratch, which the per-queue scratch reservation does not always get.
+    constexpr uint32_t kFbLaneMin = 128;
     const uint32_t nr = (uint32_t)retry.size();
     std::vector<uint32_t> rfirst{0}, ritems, rr(2 * (size_t)nr), rf(2 * (size_t)nr), rsl, rrs{0}, rset;
     for (uint32_t q = 0; q < nr; q++) {
@@ -756,7 +761,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       pr.rsig = sl.d_fb.p;
       pr.scal_tab = sl.d_fb.p + (size_t)stride * W_G2J;
       launch_sig_scale(pr, (uint32_t)rset.size(), s, sl.d_list.p + o_rset);
-      launch_group_reduce(pr, sl.d_list.p, sl.d_list.p + 2 * (size_t)nr, nr, dS, dF, s);
+      launch_group_reduce_lane(pr, sl.d_list.p, sl.d_list.p + 2 * (size_t)nr, nr, dS, dF, s);
     } else {
       sl.d_msmB.ensure((size_t)MSM_BUCKET_WORDS * std::max<uint32_t>(nrs, 1));
       sl.d_msmW.ensure((size_t)MSM_WINDOW_WORDS * nr);
@@ -765,7 +770,10 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     }
     std::vector<uint32_t> sel;  // jobs to check on their own
     if (nsub) {
-      launch_range_combine(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, s);
+      if (nsub >= kFbLaneMin)
+        launch_range_combine_lane(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, s);
+      else
+        launch_range_combine(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, s);
       launch_group_check(dS_sub, dF_sub, nsub, sl.d_ok.p + nr, s);
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpyAsync(sl.h_ok.p + nr, sl.d_ok.p + nr, nsub, hipMemcpyDeviceToHost, s));
