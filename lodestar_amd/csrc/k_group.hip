@@ -27,27 +27,11 @@ __global__ __launch_bounds__(WAVE) void k_job_mask(PipelineBuffers b) {
   for (uint32_t i = a; i < e; i++) b.include[i] = err == 0 ? 1 : 0;
 }
 
-__global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const uint32_t* set_ranges,
-                                                       const uint32_t* f_ranges, uint32_t ng, uint32_t* S_out,
+__global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const uint32_t* f_ranges, uint32_t ng,
                                                        uint32_t* F_out) {
   __shared__ uint32_t red[WAVE * W_FP12];
   const uint32_t g = blockIdx.x, lane = threadIdx.x;
   if (g >= ng) return;
-  // ---- S = sum r_i sig_i over the group's included sets (only without the MSM stage)
-  if (set_ranges) {
-    const uint32_t first = set_ranges[2 * g], last = set_ranges[2 * g + 1];
-    g2j S = jac_infinity<fp2>();
-    for (uint32_t i = first + lane; i < last; i += WAVE)
-      if (b.include[i]) S = jac_add(S, ld_g2j(b.rsig, b.n, i));
-#pragma unroll 1
-    for (int s = WAVE / 2; s >= 1; s >>= 1) {
-      if (lane >= (uint32_t)s && lane < (uint32_t)(2 * s)) st_g2j(red, WAVE, lane - s, S);
-      __syncthreads();
-      if (lane < (uint32_t)s) S = jac_add(S, ld_g2j(red, WAVE, lane));
-      __syncthreads();
-    }
-    if (lane == 0) st_g2j(S_out, ng, g, S);
-  }
   // ---- F = prod of the group's Miller chunks
   const uint32_t first = f_ranges[2 * g], last = f_ranges[2 * g + 1];
   fp12 F = fp12_one();
@@ -207,9 +191,8 @@ void launch_range_combine_lane(const uint32_t* S_in, const uint32_t* F_in, uint3
 void launch_job_mask(const PipelineBuffers& b, hipStream_t s) {
   if (b.n_jobs) hipLaunchKernelGGL(k_job_mask, grid_for(b.n_jobs), dim3(WAVE), 0, s, b);
 }
-void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
-                         uint32_t ng, uint32_t* S, uint32_t* F, hipStream_t s) {
-  if (ng) hipLaunchKernelGGL(k_group_reduce, dim3(ng), dim3(WAVE), 0, s, b, set_ranges, f_ranges, ng, S, F);
+void launch_group_reduce(const PipelineBuffers& b, const uint32_t* f_ranges, uint32_t ng, uint32_t* F, hipStream_t s) {
+  if (ng) hipLaunchKernelGGL(k_group_reduce, dim3(ng), dim3(WAVE), 0, s, b, f_ranges, ng, F);
 }
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s,
                         const uint32_t* sel, uint32_t n_sel, const uint32_t* G) {

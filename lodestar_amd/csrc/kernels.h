@@ -109,12 +109,11 @@ void launch_miller_lines(const PipelineBuffers& b, hipStream_t s);
 // Miller values of the chunks (items are units when `units`, else sets): f_chunk[c] = prod over the chunk's
 // active items of MillerLoop(P_item, H(m_item)), one lane per chunk, the Fp12 squarings shared
 void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s);
-// Batch groups: group g covers sets [set_ranges[2g], set_ranges[2g+1]) (S over included sets) and Miller
-// chunks [f_ranges[2g], f_ranges[2g+1]).
-// reduce: F_g = prod f_chunk (W_FP12 SoA, stride n_groups), and, when set_ranges is not null, S_g = sum r_i rsig_i
-// (W_G2J SoA, stride n_groups) from per-set scalings (the pipeline computes S with launch_sig_msm instead)
-void launch_group_reduce(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
-                         uint32_t n_groups, uint32_t* S, uint32_t* F, hipStream_t s);
+// Batch groups: group g covers Miller chunks [f_ranges[2g], f_ranges[2g+1]).
+// reduce: F_g = prod f_chunk over chunks [f_ranges[2g], f_ranges[2g+1]) (W_FP12 SoA, stride n_groups); S_g comes
+// from launch_sig_msm (or, in the fallback, from per-set scalings summed by launch_group_reduce_lane)
+void launch_group_reduce(const PipelineBuffers& b, const uint32_t* f_ranges, uint32_t n_groups, uint32_t* F,
+                         hipStream_t s);
 // check: ok_g = FinalExp(F_g * MillerLoop(-g1, S_g)) == 1
 // (sel: check only the entries sel[0 .. n_sel), verdict q -> ok[q])
 // (G: MillerLoop(-g1, S_g) precomputed by launch_group_sig_miller, W_FP12 SoA stride n_groups; null = computed here)

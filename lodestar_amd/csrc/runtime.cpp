@@ -638,7 +638,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   end(5, s);
   const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
   beg(6, s);
-  launch_group_reduce(pb, nullptr, d_franges, ng0, sl.d_S.p, sl.d_F.p, s);
+  launch_group_reduce(pb, d_franges, ng0, sl.d_F.p, s);
   end(6, s);
   beg(7, s);
   launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, s, nullptr, 0, sl.d_G.p);
@@ -766,7 +766,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       sl.d_msmB.ensure((size_t)MSM_BUCKET_WORDS * std::max<uint32_t>(nrs, 1));
       sl.d_msmW.ensure((size_t)MSM_WINDOW_WORDS * nr);
       launch_sig_msm(pr, sl.d_list.p + o_rsl, nrs, sl.d_list.p + o_rrs, nr, sl.d_msmB.p, sl.d_msmW.p, dS, s);
-      launch_group_reduce(pr, nullptr, sl.d_list.p + 2 * (size_t)nr, nr, dS, dF, s);
+      launch_group_reduce(pr, sl.d_list.p + 2 * (size_t)nr, nr, dF, s);
     }
     std::vector<uint32_t> sel;  // jobs to check on their own
     if (nsub) {
