@@ -107,7 +107,7 @@ struct Slot {
   // Three streams per slot: the run's independent branches overlap -- signatures + the batch tail on `stream`,
   // hash_to_G2 + Miller lines on `stream_msg`, pubkey aggregation + r_i pk_i on `stream_pk` -- joined by events.
   hipStream_t stream = nullptr, stream_msg = nullptr, stream_pk = nullptr;
-  hipEvent_t join_in = nullptr, join_msg = nullptr, join_pk = nullptr;  // no timing
+  hipEvent_t join_in = nullptr, join_msg = nullptr, join_pk = nullptr, join_mask = nullptr;  // no timing
   hipEvent_t ev[2 * (kStages + 2)] = {};  // profile: (start, end) per stage; pairs kStages, kStages + 1 = the
                                           // Miller lines, the groups' MillerLoop(-g1, S) (parts of stages 5, 7)
   // d_in / h_in: every per-call input packed into one arena (one H2D transfer); d_res / h_res: job errors +
@@ -583,10 +583,12 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.job_err = reinterpret_cast<int8_t*>(sl.d_res.p);
 
   // ---- kernel pipeline ------------------------------------------------------------------------------------
-  // DAG of one run: signatures (decode) | messages (hash_to_G2 -> affine -> Miller lines) | pubkeys (aggregate ->
-  // r_i pk_i -> affine) run on three streams after the input copy; the job mask waits for the pubkey branch,
-  // the Miller accumulation for the message branch.  An isolated call's critical path drops from the sum of
-  // the stages to hash + lines + accumulation + tail; a full chip just interleaves the branches.
+  // DAG of one run on three streams after the input copy:
+  //   signatures: decode -> [pubkeys done] job mask -> MSM -> MillerLoop(-g1, S_g) -> [Miller F done] final exp.
+  //   messages:   hash_to_G2 -> affine -> Miller lines -> [job mask done] Miller accumulation -> F reduction
+  //   pubkeys:    aggregate -> r_i pk_i -> affine
+  // An isolated call's critical path drops from the sum of the stages to the longer of the branches plus the final
+  // exponentiation; a full chip just interleaves the branches.
   const bool prof = opt.profile;
   hipStream_t sm = sl.stream_msg, sp = sl.stream_pk;
   auto beg = [&](int k, hipStream_t st) {
@@ -606,7 +608,6 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   beg(kStages, sm);
   launch_miller_lines(pb, sm);
   end(kStages, sm);
-  HIPCHK(hipEventRecord(sl.join_msg, sm));
   // pubkeys
   beg(2, sp);
   if ((table_mode || bytes_agg) && pb.n_agg) launch_pk_aggregate(pb, n, sp);
@@ -623,6 +624,18 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   HIPCHK(hipStreamWaitEvent(s, sl.join_pk, 0));
   beg(4, s);
   launch_job_mask(pb, s);
+  HIPCHK(hipEventRecord(sl.join_mask, s));
+  // the message branch continues with the Miller accumulation once the include mask exists
+  HIPCHK(hipStreamWaitEvent(sm, sl.join_mask, 0));
+  beg(5, sm);
+  if (merged) launch_unit_aggregate(pb, sm);
+  launch_miller_acc(pb, merged, sm);
+  end(5, sm);
+  const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
+  beg(6, sm);
+  launch_group_reduce(pb, d_franges, ng0, sl.d_F.p, sm);
+  end(6, sm);
+  HIPCHK(hipEventRecord(sl.join_msg, sm));
   const uint32_t* d_slices = reinterpret_cast<uint32_t*>(din + o_slices);
   const uint32_t* d_rslices = reinterpret_cast<uint32_t*>(din + o_rslices);
   launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s);
@@ -632,14 +645,6 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, s);
   end(kStages + 1, s);
   HIPCHK(hipStreamWaitEvent(s, sl.join_msg, 0));
-  beg(5, s);
-  if (merged) launch_unit_aggregate(pb, s);
-  launch_miller_acc(pb, merged, s);
-  end(5, s);
-  const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
-  beg(6, s);
-  launch_group_reduce(pb, d_franges, ng0, sl.d_F.p, s);
-  end(6, s);
   beg(7, s);
   launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, s, nullptr, 0, sl.d_G.p);
   end(7, s);
@@ -1052,7 +1057,8 @@ void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet sh
   HIPCHK(hipStreamCreateWithFlags(&s->stream_msg, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&s->stream_pk, hipStreamNonBlocking));
   s->set_stream(s->stream);
-  for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk}) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk, &s->join_mask})
+    HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
   d->slots.push_back(s);
   d->workers.emplace_back(worker_loop, d, s);
@@ -1073,7 +1079,7 @@ void destroy_device(Device* d) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);  // the stream-ordered frees
     for (auto& e : s->ev)
       if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk})
+    for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk, s->join_mask})
       if (e) (void)hipEventDestroy(e);
     for (hipStream_t st : {s->stream, s->stream_msg, s->stream_pk})
       if (st) (void)hipStreamDestroy(st);
