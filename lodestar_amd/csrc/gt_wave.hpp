@@ -501,6 +501,14 @@ __device__ void gtw_miller_loop(uint32_t* F, const uint32_t* QA, const fp& xP, c
   gtw_conj(F, F, t);
 }
 
+// Fp12 word w of the SoA tower layout in HBM (Fp2 slots c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2, W_FP words per
+// Fp) -> its word in the LDS w-basis layout of this engine
+__device__ __forceinline__ uint32_t gtw_lds_word(uint32_t w) {
+  const uint32_t slot = w / (2 * BLS_NL), rest = w % (2 * BLS_NL);
+  const uint32_t k = slot < 3 ? 2 * slot : 2 * (slot - 3) + 1;
+  return k * 2 * BLS_NL + rest;
+}
+
 // LDS footprint of one cooperative group check (words)
 struct GtwLds {
   uint32_t S[108 * BLS_NL];     // per-lane products

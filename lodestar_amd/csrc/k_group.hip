@@ -56,11 +56,6 @@ __global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const 
 //   G_in != nullptr: FinalExp(F * G) == 1 with G = MillerLoop(-g1, S) from k_group_sig_miller, which the batch
 //                    pass runs right after the MSM, beside the message branch (off the call's critical path).
 // F / G in HBM: SoA tower layout (Fp2 slots c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2); in LDS: the w-basis.
-__device__ __forceinline__ uint32_t gtw_lds_word(uint32_t w) {
-  const uint32_t slot = w / (2 * W_FP), rest = w % (2 * W_FP);
-  const uint32_t k = slot < 3 ? 2 * slot : 2 * (slot - 3) + 1;
-  return k * 2 * W_FP + rest;
-}
 // lane 0: S -> affine in QA; returns (through LDS) whether S is finite
 __device__ __forceinline__ void gtw_load_S(GtwLds& sh, const uint32_t* S_in, uint32_t ng, uint32_t g, uint32_t t) {
   if (t == 0) {

@@ -10,6 +10,7 @@
 //                   prod_i e(r_i pk_i, H(m)) = e(sum_i r_i pk_i, H(m))).
 // Line traffic is 68 x 84 words = 22.8 KB per message (HBM-cheap next to ~5,200 Montgomery products).
 #include "k_common.hpp"
+#include "gt_wave.hpp"
 
 STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_miller_lines(PipelineBuffers b) {
   uint32_t u = blockIdx.x * WAVE + threadIdx.x;
@@ -85,7 +86,47 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc(PipelineBuffers b) {
   st_fp12(b.f_chunk, b.n, c, fp12_conj(f));
 }
 
+// Small runs (latency): one 128-lane workgroup per pairing, the Miller loop as cooperative Fp12 arithmetic
+// (gt_wave.hpp: lines computed on the fly, one Fp product per lane per step) -- the same value as
+// k_miller_lines + k_miller_acc with one item per chunk, in ~1/6 of the time per pairing, at a fraction of the
+// lanes' efficiency; the runtime uses it only when the run's pairings fit the chip (runtime.cpp kCoopMaxItems).
+template <bool UNITS>
+__global__ __launch_bounds__(GTW_LANES) void k_miller_coop(PipelineBuffers b) {
+  __shared__ GtwLds sh;
+  const uint32_t c = blockIdx.x, t = threadIdx.x;
+  if (c >= b.n_chunks) return;
+  const uint32_t i = b.chunk_items[b.chunk_first[c]];  // one item per chunk
+  uint32_t m;
+  bool active;
+  if (UNITS) {
+    m = b.unit_msg[i];
+    active = b.unit_ok[i] != 0;
+  } else {
+    m = b.msg_idx[i];
+    active = b.include[i] != 0;
+  }
+  active = active && !(b.mflags[m] & MF_H_INF);  // uniform over the workgroup
+  if (active) {
+    if (t < 4) lds_st(sh.QA, (int)t, ld_fp(b.h_aff, b.nm, m, (int)t * W_FP));
+    const g1a P = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
+    gtw_sync();
+    gtw_miller_loop(sh.G, sh.QA, P.x, P.y, sh.TB, sh.L, sh.S, t);
+  } else {
+    gtw_set_one(sh.G, t);
+  }
+  gtw_sync();
+  for (uint32_t w = t; w < W_FP12; w += GTW_LANES) b.f_chunk[(size_t)w * b.n + c] = sh.G[gtw_lds_word(w)];
+}
+
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
+
+void launch_miller_coop(const PipelineBuffers& b, bool units, hipStream_t s) {
+  if (!b.n_chunks) return;
+  if (units)
+    hipLaunchKernelGGL(k_miller_coop<true>, dim3(b.n_chunks), dim3(GTW_LANES), 0, s, b);
+  else
+    hipLaunchKernelGGL(k_miller_coop<false>, dim3(b.n_chunks), dim3(GTW_LANES), 0, s, b);
+}
 
 void launch_miller_lines(const PipelineBuffers& b, hipStream_t s) {
   if (b.n_umsg) hipLaunchKernelGGL(k_miller_lines, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);

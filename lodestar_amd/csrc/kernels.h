@@ -109,6 +109,9 @@ void launch_miller_lines(const PipelineBuffers& b, hipStream_t s);
 // Miller values of the chunks (items are units when `units`, else sets): f_chunk[c] = prod over the chunk's
 // active items of MillerLoop(P_item, H(m_item)), one lane per chunk, the Fp12 squarings shared
 void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s);
+// the same for chunks of ONE item each, as one cooperative 128-lane workgroup per pairing (lines on the fly; small
+// runs, for latency)
+void launch_miller_coop(const PipelineBuffers& b, bool units, hipStream_t s);
 // Batch groups: group g covers Miller chunks [f_ranges[2g], f_ranges[2g+1]).
 // reduce: F_g = prod f_chunk over chunks [f_ranges[2g], f_ranges[2g+1]) (W_FP12 SoA, stride n_groups); S_g comes
 // from launch_sig_msm (or, in the fallback, from per-set scalings summed by launch_group_reduce_lane)
