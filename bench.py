@@ -261,7 +261,9 @@ def roofline(runs, n_sets, group_count, pubkeys_per_set, sets_per_s, miller_k=2,
         mults, ppm = stage_mults(rs, g, pubkeys_per_set, mk, nm)
         prod += np.array([mults[k] for k in STAGES]) * ppm
         ms += np.array(st_ms[:len(STAGES)])
-    best = int(np.argmax(ms))
+    # dominant kernel = the stage with the largest share of the algorithmic work (the stages of a run overlap on
+    # three streams and with other slots' runs, so their durations do not add up to the run's)
+    best = int(np.argmax(prod))
     achieved = prod[best] / (ms[best] * 1e-3) / 1e12
     n_runs = max(len(runs), 1)
     per_stage = {STAGES[k]: {"ms_per_launch": round(ms[k] / n_runs, 4),
@@ -315,8 +317,8 @@ def pmc_traffic(kernel, n_sets):
         return None
     with open(PMC_FILE) as fh:
         table = json.load(fh)["kernels"]
-    # the Miller stage is two launches per batch (k_miller.hip): line pass + accumulation pass
-    parts = {"k_miller_sets": ["k_miller_lines", "k_miller_acc"]}.get(kernel, [kernel])
+    # a stage is several launches ("k_a+k_b+..."); k_batch_inv's figure is per launch of either of its two uses
+    parts = kernel.split("+")
     if not all(p in table for p in parts):
         return None
     b16k = sum(2 * 1024 * table[p]["FETCH_SIZE_kB_per_launch"] + 1024 * table[p]["WRITE_SIZE_kB_per_launch"]
