@@ -36,6 +36,9 @@
 #ifndef BLSGPU_WPE_HASH
 #define BLSGPU_WPE_HASH BLSGPU_WPE
 #endif
+#ifndef BLSGPU_WPE_HMAP
+#define BLSGPU_WPE_HMAP BLSGPU_WPE_HASH
+#endif
 
 __device__ __forceinline__ fp ld_fp(const uint32_t* p, uint32_t n, uint32_t i, int w0) {
   fp r;

@@ -47,7 +47,7 @@ STAGE_KERNEL void k_hash_prep(PipelineBuffers b) {
 // inv: 1 / N(d) from the batch inversion; d^-1 = conj(d) / N(d).  Two lanes per message (lane pair (u, j)): each
 // runs one SSWU map + isogeny -> h_q[j] (the two maps of a message are independent, so a small call's hash
 // latency drops by one map).
-STAGE_KERNEL_W(BLSGPU_WPE_HASH) void k_hash_map(PipelineBuffers b, const uint32_t* inv) {
+STAGE_KERNEL_W(BLSGPU_WPE_HMAP) void k_hash_map(PipelineBuffers b, const uint32_t* inv) {
   const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
   if (q >= 2 * b.n_umsg) return;
   const uint32_t u = q >> 1, j = q & 1;
