@@ -317,3 +317,15 @@ extern "C" void emu_fp2_mul_lazy_limbs(const uint32_t* in56, uint32_t* out28) {
     out28[14 + i] = r.c1.l[i];
   }
 }
+// hash_to_G2 as the pipeline runs it: the two maps on separate lanes (hash_to_g2_map_j), then sum + cofactor
+// clearing (k_hash.hip k_hash_map / k_hash_clear)
+extern "C" int emu_hash_to_g2_split(const uint8_t* msg, uint8_t* out192) {
+  h2c_prep h;
+  hash_to_g2_prep(msg, h);
+  const fp2 dinv = fp2_inv(h.d);
+  const g2j Q = jac_add(hash_to_g2_map_j(h, dinv, 0), hash_to_g2_map_j(h, dinv, 1));
+  g2a a;
+  if (!jac_to_aff(clear_cofactor_g2(Q), a)) return 0;
+  g2a_to_be192(a, out192);
+  return 1;
+}

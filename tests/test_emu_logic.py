@@ -275,3 +275,14 @@ def test_fp2_mul_lazy_reduction_bounds():
         assert c0 < 1.06 * P and c1 < 1.06 * P, (vals,)
         assert c0 % P == (a0 * b0 - a1 * b1) * RINV % P, (it, vals)
         assert c1 % P == (a0 * b1 + a1 * b0) * RINV % P, (it, vals)
+
+
+def test_hash_to_g2_two_lane_split_matches_oracle():
+    """k_hash_map / k_hash_clear's split of hash_to_G2 (one SSWU map per lane, then sum and cofactor clearing)
+    against the oracle's hash_to_g2 (RFC 9380 BLS12381G2_XMD:SHA-256_SSWU_RO_ with the POP DST)."""
+    L = lib()
+    out = buf(192)
+    for j in range(6):
+        m = bytes([j * 37 % 256]) * 32 if j < 3 else random.Random(j).randbytes(32)
+        assert L.emu_hash_to_g2_split(m, out) == 1
+        assert b2g2(out.raw) == bls.hash_to_g2(m)
