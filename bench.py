@@ -46,7 +46,11 @@ def gen_keys(ctx, n):
     return sks, pks
 
 
-def gen_sigs(ctx, sk_bytes_list, msgs):
+def gen_sigs(ctx, sk_bytes_list, msgs, signer=None):
+    """Signatures sk_i H(msg_i): on the GPU (debug op 7, pinned to the oracle by tests/test_gpu_parity.py), or by
+    `signer(sks, msgs)` (the tests pass the C oracle's sign, so the inputs do not come from the device)."""
+    if signer is not None:
+        return signer(b"".join(sk_bytes_list), b"".join(msgs))
     inp = b"".join(sk + m for sk, m in zip(sk_bytes_list, msgs))
     sigs, st = ctx.debug_op(7, inp, 64, 96)
     assert (st == 0).all()
@@ -68,7 +72,7 @@ def message_variant(ctx, w, v):
     return out
 
 
-def build_workload(ctx, config, rank, world=1, n_dev=1):
+def build_workload(ctx, config, rank, world=1, n_dev=1, signer=None):
     """Returns dict of numpy inputs for verify_raw + description.  n_dev > 1: one call spans n_dev in-process
     devices (the runtime shards it), so C2 carries 16,384 sets per device."""
     if config in ("C1", "C2"):
@@ -78,11 +82,11 @@ def build_workload(ctx, config, rank, world=1, n_dev=1):
         mkeys = [rank * n + j for j in range(n)]
         msgs = [msg_j(k) for k in mkeys]
         sk_list = [sks[32 * i : 32 * i + 32] for i in range(n)]
-        sigs = gen_sigs(ctx, sk_list, msgs)
+        sigs = gen_sigs(ctx, sk_list, msgs, signer)
         w = dict(_sk=sk_list, _mkey=mkeys, _skey=mkeys,job_first_set=np.arange(n + 1, dtype=np.uint32), sigs=np.frombuffer(sigs, np.uint8),
                  sig_len=np.full(n, 96, np.uint32), msgs=np.frombuffer(b"".join(msgs), np.uint8),
                  set_pk_first=np.arange(n + 1, dtype=np.uint32), pk_index=np.arange(n, dtype=np.uint32),
-                 job_flags=np.ones(n, np.uint8), sig_stride=96, pks_table=pks)
+                 job_flags=np.ones(n, np.uint8), sig_stride=96, _table_pks=pks)
         desc = {"workload": ("C1 reference perf bench shape: 128 random single-pubkey sets per call, 1 set per batchable job"
                              if config == "C1" else
                              "C2 gossip attestation flood: 16384 single-pubkey sets per GPU, 1 set per batchable job"),
@@ -94,33 +98,35 @@ def build_workload(ctx, config, rank, world=1, n_dev=1):
         n_keys = 65536
         sks, pks = gen_keys(ctx, n_keys)
         ctx.upload_pubkeys(0, pks)
+        table_pks = pks
         mkeys = [rank * n + j for j in range(n)]
         msgs = [msg_j(k) for k in mkeys]
         agg_sks = []
         for j in range(n):
             s = sum(interop_sk(i) for i in range(512 * j, 512 * j + k)) % R_ORDER
             agg_sks.append(s.to_bytes(32, "big"))
-        sigs = gen_sigs(ctx, agg_sks, msgs)
+        sigs = gen_sigs(ctx, agg_sks, msgs, signer)
         w = dict(_sk=agg_sks, _mkey=mkeys, _skey=mkeys,job_first_set=np.array([0, n], np.uint32), sigs=np.frombuffer(sigs, np.uint8),
                  sig_len=np.full(n, 96, np.uint32), msgs=np.frombuffer(b"".join(msgs), np.uint8),
                  set_pk_first=np.arange(0, n * k + 1, k, dtype=np.uint32),
-                 pk_index=np.arange(n * k, dtype=np.uint32), job_flags=np.zeros(1, np.uint8), sig_stride=96)
+                 pk_index=np.arange(n * k, dtype=np.uint32), job_flags=np.zeros(1, np.uint8), sig_stride=96,
+                 _table_pks=table_pks)
         desc = {"workload": "C3 block import: 128 aggregate sets x 512 pubkeys (GPU aggregation), one job",
                 "sets_per_step_per_gpu": n, "pubkeys_per_set": k, "pk_mode": "device table (65536 keys)"}
         return w, n, desc, k
     if config == "C4":
-        return build_c4(ctx, rank, world)
+        return build_c4(ctx, rank, world, signer)
     if config == "C5":
-        return build_c5(ctx, rank)
+        return build_c5(ctx, rank, signer)
     raise SystemExit(f"unknown config {config}")
 
 
-def _table_workload(ctx, set_idx, set_mkey, set_sk, job_sizes, job_flags, sign_mkey=None):
+def _table_workload(ctx, set_idx, set_mkey, set_sk, job_sizes, job_flags, sign_mkey=None, signer=None):
     """Inputs for a table-mode call: set_idx[i] = pubkey indices of set i, set_sk[i] = its signing key, set i
     claims message msg_j(set_mkey[i]) and is signed over msg_j(sign_mkey[i]) (default: the claimed one)."""
     sign_mkey = set_mkey if sign_mkey is None else sign_mkey
     sk_list = [s.to_bytes(32, "big") for s in set_sk]
-    sigs = gen_sigs(ctx, sk_list, [msg_j(k) for k in sign_mkey])
+    sigs = gen_sigs(ctx, sk_list, [msg_j(k) for k in sign_mkey], signer)
     n = len(set_idx)
     spf = np.concatenate([[0], np.cumsum([len(x) for x in set_idx])]).astype(np.uint32)
     return dict(_sk=sk_list, _mkey=list(set_mkey), _skey=list(sign_mkey), job_first_set=np.concatenate([[0], np.cumsum(job_sizes)]).astype(np.uint32),
@@ -130,7 +136,7 @@ def _table_workload(ctx, set_idx, set_mkey, set_sk, job_sizes, job_flags, sign_m
                 job_flags=np.asarray(job_flags, np.uint8), sig_stride=96)
 
 
-def build_c4(ctx, rank, world):
+def build_c4(ctx, rank, world, signer=None):
     """C4 epoch scale: 2^20-validator table (replicated per GPU), 2,048 committees x 16 aggregate
     sets = 32,768 sets, committee = 512 indices with a seed-random 0-10% dropout per set, one message per
     committee, one batchable job per set.  The 32,768 sets are sharded over the ranks by
@@ -162,7 +168,8 @@ def build_c4(ctx, rank, world):
         set_msg.append(c)
         set_sk.append(sum(sk_all[int(i) % 4096] for i in idx) % R_ORDER)
     n = len(set_idx)
-    w = _table_workload(ctx, set_idx, set_msg, set_sk, [1] * n, [1] * n)
+    w = _table_workload(ctx, set_idx, set_msg, set_sk, [1] * n, [1] * n, signer=signer)
+    w["_table_pks"] = pks * reps
     desc = {"workload": f"C4 epoch scale: 32768 aggregate sets (2048 committees x 16, 512-member committees, "
                         f"0-10% dropout) over a 2^20-validator table, sharded {world} way(s)",
             "sets_per_step_per_gpu": n, "total_sets_per_step": n_sets, "pubkeys_per_set": float(np.mean([len(x) for x in set_idx])),
@@ -170,7 +177,7 @@ def build_c4(ctx, rank, world):
     return w, n, desc, int(round(desc["pubkeys_per_set"]))
 
 
-def build_c5(ctx, rank):
+def build_c5(ctx, rank, signer=None):
     """C5 mixed: 1,024 sets -- 25% proposer (single), 25% deposit-domain (single), 25%
     sync-committee contribution (aggregate <= 128), 25% sync aggregate (aggregate 512) -- in batchable jobs of
     1-3 sets, 1% of sets signed over the wrong message (-> false, invalid-batch fallback path).  Returns the
@@ -202,7 +209,9 @@ def build_c5(ctx, rank):
         k = min(left, int(rng.integers(1, 4)))
         job_sizes.append(k)
         left -= k
-    w = _table_workload(ctx, set_idx, set_msg, set_sk, job_sizes, [1] * len(job_sizes), sign_mkey=sign_keys)
+    w = _table_workload(ctx, set_idx, set_msg, set_sk, job_sizes, [1] * len(job_sizes), sign_mkey=sign_keys,
+                        signer=signer)
+    w["_table_pks"] = pks
     jfs = w["job_first_set"]
     w["expected"] = np.array([0 if any(s in bad for s in range(jfs[j], jfs[j + 1])) else 1
                               for j in range(len(job_sizes))], np.int8)
@@ -329,35 +338,106 @@ def pmc_traffic(kernel, n_sets):
 BLST_SETS_PER_CORE = 2200.0  # published anchor: ~0.9 ms/set/thread, x2 batched
 
 
-def cpu_baseline(work, expected, max_threads=16):
+def host_cpus():
+    """The host CPUs this process may use, checked rather than assumed: the affinity mask
+    (os.sched_getaffinity), its physical cores (/proc/cpuinfo physical id + core id), and the CPU share the
+    launcher grants through OMP_NUM_THREADS (the GPU box exports its per-GPU share there; os.cpu_count() is the
+    whole machine).  Threads used = the affinity count, capped by that share when one is set."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    phys, model, cur = set(), "", {}
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "processor":
+                    cur = {"cpu": int(v)}
+                elif k in ("physical id", "core id"):
+                    cur[k] = v
+                    if "physical id" in cur and "core id" in cur and cur["cpu"] in aff:
+                        phys.add((cur["physical id"], cur["core id"]))
+                elif k == "model name" and not model:
+                    model = v
+    except OSError:
+        pass
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(len(aff), share) if share > 0 else len(aff)
+    return {"threads": max(1, threads), "affinity_cpus": len(aff), "affinity_physical_cores": len(phys) or None,
+            "cpu_share_env": share or None, "os_cpu_count": os.cpu_count(), "model": model}
+
+
+def oracle_table(work):
+    from oracle import cpu
+
+    return cpu.Table(work["_table_pks"]) if "_table_pks" in work else None
+
+
+def cpu_baseline(call, expected, table, hc):
     """The reference pool restated in C (oracle/blscpu.c: 6 x 64-bit Montgomery, the pool's job split, >= 16-job
     batch chunks and per-job fallback; kind "port") on this host's cores, on the SAME step the GPU times (all of
     its sets, same inputs), with the result checked against the GPU's.  The blst pool itself cannot run here
-    (not vendored, no network): its published per-core anchor is reported beside."""
+    (not vendored, no network): its published per-core anchor is reported beside, at the threads used and at the
+    physical cores of the affinity mask."""
     from oracle import cpu
 
-    threads = max(1, min(max_threads, os.cpu_count() or 1))  # the GPU box's CPU share is 16 threads
-    call = {k: v for k, v in work.items() if k != "expected"}
-    table = cpu.Table(work["pks_table"]) if "pks_table" in work else None
-    call.pop("pks_table", None)
+    threads = hc["threads"]
     t0 = time.perf_counter()
     res, st = cpu.verify_jobs(table=table, threads=threads, **call)
     dt = time.perf_counter() - t0
-    assert np.array_equal(res, expected), "C oracle and GPU disagree on the bench step"
+    agree = bool(np.array_equal(res, expected))
     n = len(call["sig_len"])
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as fh:
-            model = next((l.split(":", 1)[1].strip() for l in fh if l.startswith("model name")), "")
-    except OSError:
-        pass
+    cores = hc["affinity_physical_cores"] or hc["affinity_cpus"]
     return {"value": round(n / dt, 2), "unit": "sets/s", "cores": threads, "kind": "port",
             "sample": f"the full bench step ({n} sets, {st.work_requests} worker requests of >= 128 sets, "
-                      f"batch chunks of >= 16 jobs) through oracle/blscpu.c on {threads} threads of '{model}' "
-                      f"(os.cpu_count() {os.cpu_count()}), {dt:.2f} s, results identical to the GPU's",
+                      f"batch chunks of >= 16 jobs) through oracle/blscpu.c on {threads} threads of '{hc['model']}', "
+                      f"{dt:.2f} s, results {'identical to' if agree else 'DIFFERENT from'} the GPU's",
+            "results_match_gpu": agree,
+            "host": {k: hc[k] for k in ("affinity_cpus", "affinity_physical_cores", "cpu_share_env", "os_cpu_count")},
             "blst_anchor_sets_per_s": BLST_SETS_PER_CORE * threads,
+            "blst_anchor_sets_per_s_affinity_cores": BLST_SETS_PER_CORE * cores,
             "blst_anchor": f"{BLST_SETS_PER_CORE:.0f} sets/s/core (reference lodestar.ts:454 ~0.9 ms/set/thread, "
-                           f"x2 batched index.ts:44) x {threads} cores; the blst pool is not runnable offline"}
+                           f"x2 batched index.ts:44) x {threads} threads used, and x {cores} physical cores of the "
+                           f"affinity mask; the blst pool is not runnable offline"}
+
+
+PARITY_SEED = SEED + 0x5041524954  # "PARIT"
+
+
+def parity_leg(ctx, work, pool, calls, expected, table, hc, slots):
+    """Untimed parity leg of the bench step: the step's sets re-signed by the ORACLE over fresh signing roots, ~1% of
+    them corrupted in every way the reference distinguishes (oracle/corrupt.py: wrong message, another set's
+    signature, negated, identity, every Signature.fromBytes error class, 48/0-byte, uncompressed), verified on the
+    GPU in the middle of 2 x slots + 2 valid in-flight calls (so a slot merges it with them, the timed region's
+    shape) and by oracle/blscpu.c on the same batch and seed; per-job mismatches are counted (reference
+    multithread.test.ts:89-106, worker.ts:76-98)."""
+    from oracle import corrupt, cpu
+
+    t0 = time.perf_counter()
+    n = len(work["_mkey"])
+    threads = hc["threads"]
+    msgs = [msg_j(k, PARITY_SEED) for k in work["_mkey"]]
+    sigs = cpu.sign(b"".join(work["_sk"]), b"".join(msgs), threads=threads)
+    rng = np.random.default_rng(PARITY_SEED & 0xFFFFFFFF)
+    msgs, sig_buf, sig_len, applied = corrupt.corrupt_sets([sigs[96 * i: 96 * i + 96] for i in range(n)], msgs, rng)
+    call = {k: v for k, v in work.items() if not k.startswith("_") and k != "expected"}
+    call.update(sigs=np.frombuffer(sig_buf, np.uint8), sig_len=np.asarray(sig_len, np.uint32),
+                msgs=np.frombuffer(b"".join(msgs), np.uint8), sig_stride=192)
+    k = 2 * slots + 2
+    valid = [pool.submit(ctx.verify_raw, **calls[1 + i % (len(calls) - 1)], seed=SEED) for i in range(k // 2)]
+    fut = pool.submit(ctx.verify_raw, **call, seed=PARITY_SEED)
+    valid += [pool.submit(ctx.verify_raw, **calls[1 + (k // 2 + i) % (len(calls) - 1)], seed=SEED) for i in range(k // 2)]
+    got, pst = fut.result()
+    valid_ok = sum(int(np.array_equal(f.result()[0], expected)) for f in valid)
+    want, ost = cpu.verify_jobs(table=table, threads=threads, **call, seed=PARITY_SEED)
+    bad = np.nonzero(got != want)[0]
+    kinds = {}
+    for i, kd in applied.items():
+        kinds[kd] = kinds.get(kd, 0) + 1
+    return {"jobs": int(len(want)), "mismatches": int(len(bad)), "first_mismatches": [int(x) for x in bad[:8]],
+            "classes": corrupt.result_classes(want), "corrupted_sets": len(applied), "corruptions": kinds,
+            "run_calls": int(pst.run_calls), "valid_calls_alongside": len(valid), "valid_calls_correct": valid_ok,
+            "oracle": f"oracle/blscpu.c verify_jobs ({threads} threads), signatures by oracle/blscpu.c sign",
+            "s": round(time.perf_counter() - t0, 2)}
 
 
 def main():
@@ -367,23 +447,21 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--group-sets", type=int, default=1024)
+    ap.add_argument("--group-policy", type=int, default=0,
+                    help="0 = batch groups of >= group-sets sets; 1 = the reference pool's jobs / requests / chunks")
     ap.add_argument("--inflight", type=int, default=32,
                     help="verifySignatureSets calls in flight per GPU (runtime slots); 1 = strictly serial")
-    ap.add_argument("--slots", type=int, default=2,
-                    help="runtime slots per GPU (0 = one per in-flight call); fewer slots than calls in flight make "
-                         "each slot merge the queued calls into one pipeline run")
+    ap.add_argument("--slots", type=int, default=0,
+                    help="runtime slots per GPU (0 = the runtime's default for the process's hardware queues); fewer "
+                         "slots than calls in flight make each slot merge the queued calls into one pipeline run")
     ap.add_argument("--merge-sets", type=int, default=131072, help="max sets of one merged pipeline run (0 = never)")
     ap.add_argument("--miller-k", type=int, default=0,
                     help="pairings per Miller accumulator (shared squarings); 0 = the runtime's choice by run size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
 
-    # Concurrent calls use one runtime slot (HIP stream) each; HIP reads GPU_MAX_HW_QUEUES once, at its first
-    # call, so the launcher sets it.  The box exports 4, which makes the slot streams share 4 in-order queues:
-    # 1.57M vs 2.23M sets/s with 8 (profiles/r02_hwq_env.json), so a smaller inherited value is raised.
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -401,12 +479,12 @@ def main():
     # one process per GPU under torch.distributed.run; without a launcher, --gpus N uses N devices in-process
     # (each call sharded over them by the runtime)
     n_dev = args.gpus if world == 1 else 1
-    if n_dev > 1 and args.config not in ("C1", "C2"):
-        raise SystemExit("in-process multi-GPU runs take --config C2 (launch other configs per rank)")
     devices = list(range(n_dev)) if world == 1 else [local_rank]
     ctx = Context(devices)
     ctx.set_option("group_sets", args.group_sets)
-    ctx.set_option("slots", max(1, args.slots or args.inflight))
+    ctx.set_option("group_policy", args.group_policy)
+    if args.slots:
+        ctx.set_option("slots", args.slots)
     ctx.set_option("merge_sets", args.merge_sets)
     ctx.set_option("miller_k", args.miller_k)
     work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev)
@@ -418,7 +496,7 @@ def main():
     t_gen = time.perf_counter()
     variants = [message_variant(ctx, work, v) for v in range(n_var)]
     t_gen = time.perf_counter() - t_gen
-    strip = lambda w: {k: v for k, v in w.items() if not k.startswith("_") and k != "pks_table"}
+    strip = lambda w: {k: v for k, v in w.items() if not k.startswith("_")}
     calls = [strip(w) for w in variants]
     call = calls[0]
 
@@ -432,7 +510,7 @@ def main():
                              f"want {expected[bad[:8]]})")
         return st, lat_ms
 
-    pool = ThreadPoolExecutor(max_workers=max(1, args.inflight))  # ctypes releases the GIL inside the call
+    pool = ThreadPoolExecutor(max_workers=max(1, args.inflight, 4 * ctx.get_option("slots") + 4))
     for _ in range(args.warmup):
         list(pool.map(step, range(max(1, args.inflight))))
     # the untimed isolated calls below use variant 0
@@ -474,6 +552,7 @@ def main():
         st_iso, l_ms = step()
         lat.append(l_ms)
     groups, n_msgs = st_iso.groups, st_iso.unique_messages  # one call alone: its own groups / distinct messages
+    runs_timed = [st for st in stats if st.run_sets > 0]
     out = {
         "metric": "verified signature sets/sec (node)",
         "miller_k": args.miller_k or "auto",
@@ -489,8 +568,10 @@ def main():
         "dtype": "u32/u64 (28-bit-limb Montgomery integer arithmetic)",
         "data": f"synthetic (interop keys, SHA-256 messages, signatures generated on the GPU before timing; "
                 f"{n_var} message variants, one per in-flight call, so merged runs share no signing root)",
-        "config": dict(desc, group_sets=args.group_sets, batch_groups_per_step=groups, inflight=args.inflight,
-                       slots=args.slots or args.inflight, merge_sets=args.merge_sets,
+        "config": dict(desc, group_sets=args.group_sets, group_policy=args.group_policy,
+                       batch_groups_per_step=groups, inflight=args.inflight,
+                       slots=ctx.get_option("slots"), hw_queues=ctx.get_option("hw_queues"),
+                       merge_sets=args.merge_sets, pipeline_runs_timed=len(runs_timed),
                        parallelism=f"shard-by-job x{n_gpus} ({'one process per GPU' if world > 1 else 'in-process devices'}), no collective"),
         "p50_batch_latency_ms": round(float(np.median(lat)), 3),
         "call_latency_under_load_ms": {"p50": round(float(np.percentile(call_lat, 50)), 2),
@@ -498,7 +579,7 @@ def main():
     }
     if not args.no_profile:
         runs = [(list(st.stage_ms[:8]), st.run_sets, st.groups, st.unique_messages // n_dev, miller_k_of(st))
-                for st in stats if st.run_sets > 0 and n_dev == 1]
+                for st in runs_timed if n_dev == 1]
         ctx.set_option("profile", 1)
         stage_acc = np.zeros(8)
         for _ in range(2):
@@ -507,9 +588,13 @@ def main():
         ctx.set_option("profile", 0)
         out["roofline"] = roofline(runs, n_sets // n_dev, groups // n_dev, pk_per_set, value / n_gpus,
                                    miller_k_of(st_p), n_msgs // n_dev, isolated=stage_acc / 2)
-    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(dict(call, pks_table=work["pks_table"]) if "pks_table" in work else call,
-                                           expected)
+    if rank == 0 and n_gpus == 1 and not (args.no_cpu_baseline and args.no_parity):
+        hc = host_cpus()
+        table = oracle_table(work)
+        if not args.no_parity:
+            out["parity"] = parity_leg(ctx, work, pool, calls, expected, table, hc, ctx.get_option("slots"))
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(call, expected, table, hc)
     out["workload_variants"] = {"count": n_var, "gen_s": round(t_gen, 2)}
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define BLSGPU_ABI_VERSION 3
+#define BLSGPU_ABI_VERSION 4
 
 enum blsgpu_code {
   BLSGPU_OK = 0,
@@ -104,13 +104,16 @@ typedef struct blsgpu_stats {
   uint32_t miller_chunks;   /* Miller accumulators of the batch pass (miller_k pairings share squarings) */
   uint32_t run_sets;        /* sets of the pipeline run that stage_ms timed: a runtime slot that merged queued
                                calls into one run reports it (and stage_ms) on the first call, 0 on the others */
+  uint32_t run_calls;       /* calls served by the pipeline run of this call's (first) shard: 1 = ran alone, k > 1 =
+                               merged with k - 1 other queued calls (set on every call of the run) */
 } blsgpu_stats;
 
-/* Create a context on the given HIP devices (NULL / n <= 0: every visible device).  Each device gets 4
- * runtime slots (option "slots"), each a HIP stream served by one long-lived dispatcher thread; concurrent
- * calls run on different slots.  Streams sharing an in-order hardware queue serialize, so the launcher
- * should set GPU_MAX_HW_QUEUES >= slots before the process's first HIP call (the library does not touch
- * the environment). */
+/* Create a context on the given HIP devices (NULL / n <= 0: every visible device).  Each device runs
+ * "slots" runtime slots (a slot = its HIP streams + staging, served by one long-lived dispatcher thread);
+ * concurrent calls run on different slots.  Slots are created by the first call, so a "slots" value set right
+ * after init is the count the device runs; later changes add or retire slots.  The library never touches the
+ * environment: HIP maps the slots' streams onto GPU_MAX_HW_QUEUES hardware queues (HIP's default 4), and the
+ * default slot count is chosen so the streams fit the queues the process has (blsgpu_get_option "hw_queues"). */
 int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out);
 /* Waits for in-flight submissions, fails queued ones with BLSGPU_ERR_CLOSED, frees everything. */
 void blsgpu_destroy(blsgpu_ctx* ctx);
@@ -137,14 +140,27 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
                   blsgpu_done_cb done, void* user);
 
 /* Tunables: "group_sets" (sets per batch group before a new one opens, default 1024), "slots" (runtime slots
- * per device, only grows, default 4), "max_devices" (devices one call may shard over, default all),
+ * per device, 1..64; default by hardware queues), "max_devices" (devices one call may shard over, default all),
  * "dedupe" (message dedupe + same-message pairing, 0/1, default 1), "miller_k" (pairings per Miller
  * accumulator sharing its Fp12 squarings, 1..64; default 0 = by run size: 1 below 32768 sets, 2 below 65536,
  * else 4), "merge_sets" (a runtime slot merges calls
  * already queued on its device into one pipeline run of up to this many sets -- jobs and results stay per
  * call -- default 65536, 0 = never), "profile" (per-stage kernel times in
- * blsgpu_stats.stage_ms, 0/1).  Applies to calls submitted afterwards. */
+ * blsgpu_stats.stage_ms, 0/1), "group_policy" (0 = batch groups of >= group_sets sets, the default; 1 = the
+ * reference pool's grouping: calls split into <= 128-set jobs (chunkifyMaximizeChunkSize(sets, 128),
+ * multithread/index.ts:156), packed into >= 128-set worker requests (prepareWork, index.ts:386-401), each
+ * request's batchable jobs checked in chunks of >= 16 jobs (worker.ts:17,56), so batch_retries and
+ * batch_sigs_success count the reference's units).  Applies to calls submitted afterwards. */
 int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value);
+/* Current value of a tunable (the keys of blsgpu_set_option; "slots" = the slots device 0 runs, or will create
+ * on the first call) or of a read-only property: "hw_queues" (the GPU_MAX_HW_QUEUES HIP runs with),
+ * "abi_version". */
+int blsgpu_get_option(const blsgpu_ctx* ctx, const char* key, int64_t* value);
+
+/* chunkifyMaximizeChunkSize(arr of len items, min_per_chunk) (multithread/utils.ts:4-19): writes the first
+ * index of every chunk and len to chunk_first[0 .. *n_chunks] (room for len / min_per_chunk + 2 entries).
+ * Pure host code; the rule group_policy 1 applies. */
+int blsgpu_chunkify(uint32_t len, uint32_t min_per_chunk, uint32_t* chunk_first, uint32_t* n_chunks);
 
 /* PublicKey.aggregate(set pubkeys).toBytes() for every set of `b` (only n_sets and the pubkey fields are
  * read; any of the three modes): out[out_len * i], out_len 96 (uncompressed) or 48 (compressed);

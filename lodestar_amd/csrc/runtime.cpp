@@ -116,6 +116,7 @@ struct Slot {
   DevBuf<uint32_t> d_work, d_lines, d_S, d_F, d_G, d_list, d_msmB, d_msmW, d_fb;
   HostBuf<uint8_t> h_in, h_res, h_ok;
   HostBuf<uint32_t> h_list;
+  bool retire = false;  // set under the device queue lock: the dispatcher exits instead of taking work
 
   void set_stream(hipStream_t st) {
     for (auto* b : {&d_in, &d_res, &d_bytes, &d_ok}) b->st = st;
@@ -169,9 +170,25 @@ struct Options {  // snapshot taken at the start of each call
   bool dedupe = true;
   int64_t miller_k = 0;  // pairings per Miller accumulator (shared squarings); 0 = by run size (miller_k_auto)
   int64_t merge_sets = 65536;  // queued calls a slot merges into one pipeline run (sets), 0 = never
+  int64_t group_policy = 0;    // 0 = groups of >= group_sets sets; 1 = the reference pool's jobs / requests / chunks
   bool same_run(const struct Options& o) const {
-    return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k;
+    return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
+           group_policy == o.group_policy;
   }
+};
+
+// chunkifyMaximizeChunkSize (reference multithread/utils.ts:4-19): floor(len / min) chunks of ceil(len / count)
+// items, or one chunk when that count is <= 1.  Returns the items per chunk.
+inline uint32_t chunk_size(uint32_t len, uint32_t min_per_chunk) {
+  const uint32_t count = min_per_chunk ? len / min_per_chunk : 0;
+  return count <= 1 ? len : (len + count - 1) / count;
+}
+
+// A batch group: jobs [first, end) of the (shard-relative) job list; `batchable` = a chunk of batchable jobs (the
+// reference's batch attempt, counted by the batchRetries / batchSigsSuccess metrics).
+struct GroupPlanEntry {
+  uint32_t first, end;
+  bool batchable;
 };
 
 // Pairings per Miller accumulator when the option is 0: shared squarings save work (k = 4: 3,483 products per
@@ -250,7 +267,10 @@ struct blsgpu_ctx {
   std::mutex table_mu;  // serializes uploads
   std::mutex opt_mu;
   Options opt;
-  int64_t slots_per_device = 4;
+  int64_t slots_per_device = 2;  // set at init from the hardware queues (default_slots)
+  int64_t hw_queues = 4;
+  std::mutex slots_mu;  // slot creation / resizing
+  bool slots_started = false;
 };
 
 namespace {
@@ -317,8 +337,12 @@ struct MsgIndex {
 };
 
 // Runs one device's shard on one slot.  Writes job_result[job_begin..job_end).
+// With `plan` (group_policy 1), the groups are the plan's job ranges instead of >= group_sets packing, and the
+// batchRetries / batchSigsSuccess metrics count the plan's batchable chunks the way the worker does (worker.ts:
+// 56-84: a chunk that throws or returns false is one retry; a chunk that verifies adds all its sets).
 int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_t* job_result, uint64_t seed,
-              const Options& opt, uint32_t max_index, blsgpu_stats& st, const uint64_t* scal_words = nullptr) {
+              const Options& opt, uint32_t max_index, blsgpu_stats& st, const uint64_t* scal_words = nullptr,
+              const std::vector<GroupPlanEntry>* plan = nullptr) {
   const uint32_t n = sh.set_end - sh.set_begin;
   const uint32_t nj = sh.job_end - sh.job_begin;
   if (nj == 0) return BLSGPU_OK;
@@ -336,7 +360,18 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // ---- host-side job structure: groups (contiguous job ranges), scalars ------------------------------------
   std::vector<uint64_t> scal(n);
   std::vector<std::pair<uint32_t, uint32_t>> group_jobs;  // [first job, end job) (shard-relative)
-  {
+  std::vector<uint8_t> group_batchable;                   // plan only: the group is a batchable chunk
+  if (plan) {
+    for (const GroupPlanEntry& g : *plan) {
+      uint32_t sets = 0;
+      for (uint32_t j = g.first; j < g.end; j++)
+        sets += b.job_first_set[sh.job_begin + j + 1] - b.job_first_set[sh.job_begin + j];
+      if (!sets) continue;  // empty jobs are rejected by the job mask, they join no group
+      group_jobs.push_back({g.first, g.end});
+      group_batchable.push_back(g.batchable);
+    }
+    // scalars come from scal_words (the caller applies shard_scalars' rule in the calls' own set order)
+  } else {
     uint32_t cur_sets = 0;
     bool open = false;
     for (uint32_t j = 0; j < nj; j++) {
@@ -689,7 +724,25 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     std::vector<uint32_t> clean;
     for (uint32_t j = group_jobs[g].first; j < group_jobs[g].second; j++)
       if (jr[j] == 2) clean.push_back(j);
+    if (plan) {  // the worker's metrics: a chunk with a throwing job or a failed equation is one retry
+      if (!group_batchable[g]) {
+      } else if (clean.size() == group_jobs[g].second - group_jobs[g].first && sl.h_res.p[o_ok + g]) {
+        st.batch_sigs_success += job_sets(group_jobs[g].second - 1).second - job_sets(group_jobs[g].first).first;
+      } else {
+        st.batch_retries++;
+      }
+    }
     if (clean.empty()) continue;
+    if (plan) {
+      if (sl.h_res.p[o_ok + g]) {
+        for (uint32_t j : clean) jr[j] = 1;
+      } else if (clean.size() == 1) {
+        jr[clean[0]] = 0;
+      } else {
+        retry.insert(retry.end(), clean.begin(), clean.end());
+      }
+      continue;
+    }
     if (sl.h_res.p[o_ok + g]) {
       for (uint32_t j : clean) jr[j] = 1;
       if (group_jobs[g].second - group_jobs[g].first > 1)
@@ -872,6 +925,7 @@ void finish_call(Call* c) {
     if (c->rc[k] != BLSGPU_OK && c->rc[k] != BLSGPU_DEVICE_ERROR) status = c->rc[k];
   }
   local.run_sets = c->sst.empty() ? 0 : c->sst[0].run_sets;
+  local.run_calls = c->sst.empty() ? 0 : c->sst[0].run_calls;
   local.devices_used = (uint32_t)c->shards.size();
   local.device_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->t0).count();
   if (c->stats) *c->stats = local;
@@ -887,7 +941,11 @@ void finish_call(Call* c) {
     void* user = c->user;
     delete c->owned;
     delete c;
-    if (done) done(user, status);
+    // a throwing callback must not unwind the dispatcher thread (std::terminate would take the host process down)
+    if (done) try {
+        done(user, status);
+      } catch (...) {
+      }
   }
   leave(ctx);
 }
@@ -906,93 +964,255 @@ void shard_scalars(const blsgpu_batch& b, const Shard& sh, uint64_t seed, uint64
   }
 }
 
+// group_policy 1: the reference pool's grouping on the GPU.  A call's sets are split into jobs of <= 128 sets
+// (chunkifyMaximizeChunkSize(sets, 128), multithread/index.ts:156), consecutive jobs are packed into worker requests
+// of >= 128 sets (prepareWork, index.ts:386-401), and each request's batchable jobs are checked in chunks of >= 16
+// jobs, its other jobs one by one (worker.ts:40-92).  The jobs are laid out group after group (one permuted batch),
+// run as one pipeline with that group plan, and each call gets the first rejection of its jobs in job order, else
+// false if a job is false, else true (Promise.all over the call's jobs, index.ts:165-173; oracle/blscpu.c
+// blscpu_verify_jobs applies the same rule).
+int run_pool_policy(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_t* job_result, uint64_t seed,
+                    const Options& opt, uint32_t max_index, blsgpu_stats& st, const uint64_t* scal_words) {
+  const uint32_t s0 = sh.set_begin, n = sh.set_end - sh.set_begin;
+  std::vector<uint64_t> scal0(std::max<uint32_t>(n, 1));
+  if (scal_words)
+    memcpy(scal0.data(), scal_words, (size_t)n * 8);
+  else
+    shard_scalars(b, sh, seed, scal0.data());
+  struct Sub {
+    uint32_t call, a, e;
+    bool batchable;
+  };
+  std::vector<Sub> subs;
+  for (uint32_t j = sh.job_begin; j < sh.job_end; j++) {
+    const uint32_t a = b.job_first_set[j], e = b.job_first_set[j + 1];
+    const bool bt = b.job_flags && (b.job_flags[j] & 1u);
+    if (a == e) {
+      subs.push_back({j, a, a, bt});
+      continue;
+    }
+    const uint32_t per = chunk_size(e - a, 128);
+    for (uint32_t k = a; k < e; k += per) subs.push_back({j, k, std::min(e, k + per), bt});
+  }
+  std::vector<uint32_t> order;  // sub-job indices in group order
+  std::vector<GroupPlanEntry> plan;
+  for (size_t q = 0; q < subs.size();) {
+    size_t q1 = q;
+    uint32_t total = 0;
+    while (q1 < subs.size() && total < 128) total += subs[q1].e - subs[q1].a, q1++;
+    std::vector<uint32_t> bat, rest;
+    for (size_t x = q; x < q1; x++) (subs[x].batchable && subs[x].e > subs[x].a ? bat : rest).push_back((uint32_t)x);
+    if (!bat.empty()) {
+      const uint32_t per = chunk_size((uint32_t)bat.size(), 16);
+      for (size_t k = 0; k < bat.size(); k += per) {
+        GroupPlanEntry g{(uint32_t)order.size(), 0, true};
+        for (size_t x = k; x < std::min(bat.size(), k + per); x++) order.push_back(bat[x]);
+        g.end = (uint32_t)order.size();
+        plan.push_back(g);
+      }
+    }
+    for (uint32_t x : rest) {
+      plan.push_back({(uint32_t)order.size(), (uint32_t)order.size() + 1, false});
+      order.push_back(x);
+    }
+    q = q1;
+  }
+  const int mode = pk_mode(b);
+  const uint32_t ns = (uint32_t)subs.size();
+  std::vector<uint32_t> jfs{0}, siglen, spf{0}, pki;
+  std::vector<uint8_t> flags, msgs, sigs, pkb;
+  std::vector<uint64_t> scal;
+  jfs.reserve(ns + 1);
+  siglen.reserve(n);
+  scal.reserve(n);
+  msgs.reserve((size_t)n * 32);
+  sigs.reserve((size_t)n * b.sig_stride);
+  for (uint32_t x : order) {
+    const Sub& u = subs[x];
+    jfs.push_back(jfs.back() + u.e - u.a);
+    flags.push_back(u.batchable ? 1 : 0);
+    for (uint32_t i = u.a; i < u.e; i++) {
+      siglen.push_back(b.sig_len[i]);
+      sigs.insert(sigs.end(), b.sigs + (size_t)i * b.sig_stride, b.sigs + (size_t)(i + 1) * b.sig_stride);
+      msgs.insert(msgs.end(), b.msgs + (size_t)i * 32, b.msgs + (size_t)i * 32 + 32);
+      scal.push_back(scal0[i - s0]);
+      if (mode == 1) {
+        pkb.insert(pkb.end(), b.pk_bytes + (size_t)i * 96, b.pk_bytes + (size_t)(i + 1) * 96);
+      } else {
+        const uint32_t k0 = b.set_pk_first[i], k1 = b.set_pk_first[i + 1];
+        spf.push_back(spf.back() + k1 - k0);
+        if (mode == 0)
+          pki.insert(pki.end(), b.pk_index + k0, b.pk_index + k1);
+        else
+          pkb.insert(pkb.end(), b.pk_bytes + (size_t)k0 * 96, b.pk_bytes + (size_t)k1 * 96);
+      }
+    }
+  }
+  blsgpu_batch pb{};
+  pb.n_sets = n;
+  pb.n_jobs = ns;
+  pb.job_first_set = jfs.data();
+  pb.job_flags = flags.data();
+  pb.pk_bytes = mode ? pkb.data() : nullptr;
+  pb.set_pk_first = mode == 1 ? nullptr : spf.data();
+  pb.pk_index = mode == 0 ? pki.data() : nullptr;
+  pb.msgs = msgs.data();
+  pb.sigs = sigs.data();
+  pb.sig_len = siglen.data();
+  pb.sig_stride = b.sig_stride;
+  std::vector<int8_t> sub_res(std::max<uint32_t>(ns, 1), 0);
+  const Shard all{0, ns, 0, n};
+  const int rc = run_shard(d, sl, pb, all, sub_res.data(), seed, opt, max_index, st, scal.data(), &plan);
+  if (rc != BLSGPU_OK) return rc;
+  std::vector<uint32_t> pos(ns);
+  for (uint32_t k = 0; k < ns; k++) pos[order[k]] = k;
+  std::vector<uint8_t> seen(sh.job_end - sh.job_begin, 0);
+  for (uint32_t j = sh.job_begin; j < sh.job_end; j++) job_result[j] = 1;
+  for (uint32_t x = 0; x < ns; x++) {
+    const uint32_t call = subs[x].call;
+    const int8_t r = sub_res[pos[x]];
+    if (seen[call - sh.job_begin]) continue;
+    if (r < 0) {
+      job_result[call] = r;
+      seen[call - sh.job_begin] = 1;
+    } else if (r == 0) {
+      job_result[call] = 0;
+    }
+  }
+  return BLSGPU_OK;
+}
+
+// One shard of a call (or a merged batch) under the call's group policy.
+int run_call_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_t* job_result, uint64_t seed,
+                   const Options& opt, uint32_t max_index, blsgpu_stats& st, const uint64_t* scal_words = nullptr) {
+  if (opt.group_policy == 1) return run_pool_policy(d, sl, b, sh, job_result, seed, opt, max_index, st, scal_words);
+  return run_shard(d, sl, b, sh, job_result, seed, opt, max_index, st, scal_words);
+}
+
+// Does the device's table hold every index the call's shard uses?  (Checked per device under its table lock: a
+// call may race an upload that has reached some devices only.)
+inline bool table_covers(const Device& d, const Call* c, const Shard& sh) {
+  const blsgpu_batch& b = c->b;
+  if (b.pk_bytes || !b.set_pk_first || sh.set_end == sh.set_begin) return true;
+  if (b.set_pk_first[sh.set_end] == b.set_pk_first[sh.set_begin]) return true;
+  return c->max_index < d.table_n;
+}
+
 // Several queued shards (of different calls) run as ONE pipeline: their inputs are concatenated into one
 // batch (jobs and results stay per call), so a launch fills the chip instead of one call's 16k-set share --
 // the device-side counterpart of the pool packing queued jobs into one worker request (prepareWork,
-// multithread/index.ts:386-401).  Jobs never interact, so every job's result is the one it gets alone.
-int run_merged(Device& d, Slot& sl, const std::vector<Task>& parts, std::vector<int>& rcs) {
-  const Call* c0 = parts[0].call;
-  const int mode = pk_mode(c0->b);
-  uint32_t n = 0, nj = 0, npk = 0, max_index = 0;
-  for (const Task& t : parts) {
-    const Shard& sh = t.call->shards[t.shard];
-    const blsgpu_batch& b = t.call->b;
-    n += sh.set_end - sh.set_begin;
-    nj += sh.job_end - sh.job_begin;
-    if (b.set_pk_first) npk += b.set_pk_first[sh.set_end] - b.set_pk_first[sh.set_begin];
-    max_index = std::max(max_index, t.call->max_index);
+// multithread/index.ts:386-401).  Jobs never interact, so every job's result is the one it gets alone.  A call
+// that cannot run (a table index beyond the device's table) is completed with ERR_ARGS on its own and never
+// joins the run; a failure of the run completes its calls with DEVICE_ERROR (every job rejected, never `false`).
+// The caller holds the device's table lock (shared).
+void run_merged(Device& d, Slot& sl, const std::vector<Task>& parts, std::vector<int>& rcs) {
+  std::vector<size_t> live;
+  for (size_t p = 0; p < parts.size(); p++) {
+    const Call* c = parts[p].call;
+    if (c->ctx->closed && !c->sync)
+      rcs[p] = BLSGPU_ERR_CLOSED;
+    else if (!table_covers(d, c, c->shards[parts[p].shard]))
+      rcs[p] = BLSGPU_ERR_ARGS;
+    else
+      live.push_back(p);
   }
-  std::vector<uint32_t> jfs{0}, siglen, spf{0}, pki;
-  std::vector<uint8_t> flags, pkb, msgs, sigs;
-  std::vector<uint64_t> scal(n);
-  jfs.reserve(nj + 1);
-  siglen.reserve(n);
-  msgs.reserve((size_t)n * 32);
-  sigs.reserve((size_t)n * 192);
-  if (mode == 0) pki.reserve(npk);
-  if (mode == 1) pkb.reserve((size_t)n * 96);
-  if (mode == 2) pkb.reserve((size_t)npk * 96);
-  uint32_t so = 0;
-  for (const Task& t : parts) {
-    const Shard& sh = t.call->shards[t.shard];
-    const blsgpu_batch& b = t.call->b;
-    shard_scalars(b, sh, t.call->seed, scal.data() + so);
-    for (uint32_t j = sh.job_begin; j < sh.job_end; j++) {
-      jfs.push_back(so + b.job_first_set[j + 1] - sh.set_begin);
-      flags.push_back(b.job_flags ? b.job_flags[j] : 0);
-    }
-    for (uint32_t i = sh.set_begin; i < sh.set_end; i++) {
-      const uint32_t len = b.sig_len[i];
-      siglen.push_back(len);
-      const size_t at = sigs.size();
-      sigs.resize(at + 192, 0);
-      if (len == 96 || len == 192) memcpy(sigs.data() + at, b.sigs + (size_t)i * b.sig_stride, len);
-    }
-    msgs.insert(msgs.end(), b.msgs + (size_t)sh.set_begin * 32, b.msgs + (size_t)sh.set_end * 32);
-    if (mode == 1) {
-      pkb.insert(pkb.end(), b.pk_bytes + (size_t)sh.set_begin * 96, b.pk_bytes + (size_t)sh.set_end * 96);
-    } else {
-      const uint32_t k0 = b.set_pk_first[sh.set_begin];
-      for (uint32_t i = sh.set_begin; i < sh.set_end; i++) spf.push_back(spf.back() + b.set_pk_first[i + 1] - b.set_pk_first[i]);
-      if (mode == 0)
-        pki.insert(pki.end(), b.pk_index + k0, b.pk_index + b.set_pk_first[sh.set_end]);
-      else
-        pkb.insert(pkb.end(), b.pk_bytes + (size_t)k0 * 96, b.pk_bytes + (size_t)b.set_pk_first[sh.set_end] * 96);
-    }
-    so += sh.set_end - sh.set_begin;
-  }
-  blsgpu_batch mb{};
-  mb.n_sets = n;
-  mb.n_jobs = nj;
-  mb.job_first_set = jfs.data();
-  mb.job_flags = flags.data();
-  mb.pk_bytes = mode ? pkb.data() : nullptr;
-  mb.set_pk_first = mode == 1 ? nullptr : spf.data();
-  mb.pk_index = mode == 0 ? pki.data() : nullptr;
-  mb.msgs = msgs.data();
-  mb.sigs = sigs.data();
-  mb.sig_len = siglen.data();
-  mb.sig_stride = 192;
-  std::vector<int8_t> res(nj, 0);
+  if (live.empty()) return;
+  int rc = BLSGPU_OK;
   blsgpu_stats st{};
-  const Shard all{0, nj, 0, n};
-  int rc;
+  std::vector<int8_t> res;
   try {
-    rc = run_shard(d, sl, mb, all, res.data(), c0->seed, c0->opt, max_index, st, scal.data());
+    const Call* c0 = parts[live[0]].call;
+    const int mode = pk_mode(c0->b);
+    uint32_t n = 0, nj = 0, npk = 0, max_index = 0;
+    for (size_t p : live) {
+      const Task& t = parts[p];
+      const Shard& sh = t.call->shards[t.shard];
+      const blsgpu_batch& b = t.call->b;
+      n += sh.set_end - sh.set_begin;
+      nj += sh.job_end - sh.job_begin;
+      if (b.set_pk_first) npk += b.set_pk_first[sh.set_end] - b.set_pk_first[sh.set_begin];
+      max_index = std::max(max_index, t.call->max_index);
+    }
+    std::vector<uint32_t> jfs{0}, siglen, spf{0}, pki;
+    std::vector<uint8_t> flags, pkb, msgs, sigs;
+    std::vector<uint64_t> scal(std::max<uint32_t>(n, 1));
+    jfs.reserve(nj + 1);
+    siglen.reserve(n);
+    msgs.reserve((size_t)n * 32);
+    sigs.reserve((size_t)n * 192);
+    if (mode == 0) pki.reserve(npk);
+    if (mode == 1) pkb.reserve((size_t)n * 96);
+    if (mode == 2) pkb.reserve((size_t)npk * 96);
+    uint32_t so = 0;
+    for (size_t p : live) {
+      const Task& t = parts[p];
+      const Shard& sh = t.call->shards[t.shard];
+      const blsgpu_batch& b = t.call->b;
+      shard_scalars(b, sh, t.call->seed, scal.data() + so);
+      for (uint32_t j = sh.job_begin; j < sh.job_end; j++) {
+        jfs.push_back(so + b.job_first_set[j + 1] - sh.set_begin);
+        flags.push_back(b.job_flags ? b.job_flags[j] : 0);
+      }
+      for (uint32_t i = sh.set_begin; i < sh.set_end; i++) {
+        const uint32_t len = b.sig_len[i];
+        siglen.push_back(len);
+        const size_t at = sigs.size();
+        sigs.resize(at + 192, 0);
+        if (len == 96 || len == 192) memcpy(sigs.data() + at, b.sigs + (size_t)i * b.sig_stride, len);
+      }
+      msgs.insert(msgs.end(), b.msgs + (size_t)sh.set_begin * 32, b.msgs + (size_t)sh.set_end * 32);
+      if (mode == 1) {
+        pkb.insert(pkb.end(), b.pk_bytes + (size_t)sh.set_begin * 96, b.pk_bytes + (size_t)sh.set_end * 96);
+      } else {
+        const uint32_t k0 = b.set_pk_first[sh.set_begin];
+        for (uint32_t i = sh.set_begin; i < sh.set_end; i++)
+          spf.push_back(spf.back() + b.set_pk_first[i + 1] - b.set_pk_first[i]);
+        if (mode == 0)
+          pki.insert(pki.end(), b.pk_index + k0, b.pk_index + b.set_pk_first[sh.set_end]);
+        else
+          pkb.insert(pkb.end(), b.pk_bytes + (size_t)k0 * 96, b.pk_bytes + (size_t)b.set_pk_first[sh.set_end] * 96);
+      }
+      so += sh.set_end - sh.set_begin;
+    }
+    blsgpu_batch mb{};
+    mb.n_sets = n;
+    mb.n_jobs = nj;
+    mb.job_first_set = jfs.data();
+    mb.job_flags = flags.data();
+    mb.pk_bytes = mode ? pkb.data() : nullptr;
+    mb.set_pk_first = mode == 1 ? nullptr : spf.data();
+    mb.pk_index = mode == 0 ? pki.data() : nullptr;
+    mb.msgs = msgs.data();
+    mb.sigs = sigs.data();
+    mb.sig_len = siglen.data();
+    mb.sig_stride = 192;
+    res.assign(std::max<uint32_t>(nj, 1), 0);
+    const Shard all{0, nj, 0, n};
+    rc = run_call_shard(d, sl, mb, all, res.data(), c0->seed, c0->opt, max_index, st, scal.data());
   } catch (...) {
     rc = BLSGPU_DEVICE_ERROR;
   }
+  st.run_calls = (uint32_t)live.size();
   uint32_t jo = 0;
-  for (size_t p = 0; p < parts.size(); p++) {
+  for (size_t k = 0; k < live.size(); k++) {
+    const size_t p = live[k];
     Call* c = parts[p].call;
     const Shard& sh = c->shards[parts[p].shard];
-    for (uint32_t j = sh.job_begin; j < sh.job_end; j++)
-      c->job_result[j] = rc == BLSGPU_DEVICE_ERROR ? -BLSGPU_DEVICE_ERROR : res[jo++];
-    if (rc == BLSGPU_DEVICE_ERROR) jo += sh.job_end - sh.job_begin;
-    if (p == 0) c->sst[parts[p].shard] = st;  // the merged run's counters go to its first call
+    for (uint32_t j = sh.job_begin; j < sh.job_end; j++, jo++) {
+      if (rc == BLSGPU_OK)
+        c->job_result[j] = res[jo];
+      else if (rc == BLSGPU_DEVICE_ERROR)  // a device failure rejects every job, never `false`
+        c->job_result[j] = -BLSGPU_DEVICE_ERROR;
+    }
+    blsgpu_stats& cs = c->sst[parts[p].shard];
+    if (k == 0) {
+      cs = st;  // the merged run's counters (and stage times) go to its first call
+    } else {
+      cs = blsgpu_stats{};
+      cs.run_calls = st.run_calls;
+    }
     rcs[p] = rc;
   }
-  return rc;
 }
 
 void run_task(Device& d, Slot& sl, const Task& t) {
@@ -1004,7 +1224,12 @@ void run_task(Device& d, Slot& sl, const Task& t) {
   } else {
     try {
       std::shared_lock<std::shared_mutex> tl(d.table_mu);
-      rc = run_shard(d, sl, c->b, sh, c->job_result, c->seed, c->opt, c->max_index, c->sst[t.shard]);
+      if (!table_covers(d, c, sh)) {
+        rc = BLSGPU_ERR_ARGS;
+      } else {
+        rc = run_call_shard(d, sl, c->b, sh, c->job_result, c->seed, c->opt, c->max_index, c->sst[t.shard]);
+        c->sst[t.shard].run_calls = 1;
+      }
     } catch (...) {
       rc = BLSGPU_DEVICE_ERROR;
     }
@@ -1020,13 +1245,17 @@ inline uint32_t task_sets(const Task& t) {
   return sh.set_end - sh.set_begin;
 }
 
+// A slot's dispatcher: takes the oldest queued shard of its device, merges the compatible shards queued behind it
+// (up to merge_sets sets), runs them, completes their calls.  Exits when the device stops (queue drained) or when
+// the slot is retired (option "slots" lowered).
 void worker_loop(Device* d, Slot* sl) {
   (void)hipSetDevice(d->id);
   for (;;) {
     std::vector<Task> parts;
     {
       std::unique_lock<std::mutex> lk(d->q_mu);
-      d->q_cv.wait(lk, [&] { return d->stop || !d->queue.empty(); });
+      d->q_cv.wait(lk, [&] { return d->stop || sl->retire || !d->queue.empty(); });
+      if (sl->retire) return;
       if (d->queue.empty()) return;  // stop requested and nothing left
       parts.push_back(d->queue.front());
       d->queue.pop_front();
@@ -1049,9 +1278,15 @@ void worker_loop(Device* d, Slot* sl) {
       continue;
     }
     std::vector<int> rcs(parts.size(), BLSGPU_OK);
-    {
+    try {
       std::shared_lock<std::shared_mutex> tl(d->table_mu);
       run_merged(*d, *sl, parts, rcs);
+    } catch (...) {  // run_merged catches its own failures; this only guards the lock
+      for (size_t p = 0; p < parts.size(); p++) {
+        const Shard& sh = parts[p].call->shards[parts[p].shard];
+        for (uint32_t j = sh.job_begin; j < sh.job_end; j++) parts[p].call->job_result[j] = -BLSGPU_DEVICE_ERROR;
+        rcs[p] = BLSGPU_DEVICE_ERROR;
+      }
     }
     for (size_t p = 0; p < parts.size(); p++) {
       Call* c = parts[p].call;
@@ -1061,18 +1296,61 @@ void worker_loop(Device* d, Slot* sl) {
   }
 }
 
+// Frees a slot whose dispatcher has exited (or never started).
+void free_slot(Device* d, Slot* s) {
+  (void)hipSetDevice(d->id);
+  for (hipStream_t st : {s->stream, s->stream_msg, s->stream_pk})
+    if (st) (void)hipStreamSynchronize(st);
+  s->release_all();
+  if (s->stream) (void)hipStreamSynchronize(s->stream);  // the stream-ordered frees
+  for (auto& e : s->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk, s->join_mask})
+    if (e) (void)hipEventDestroy(e);
+  for (hipStream_t st : {s->stream, s->stream_msg, s->stream_pk})
+    if (st) (void)hipStreamDestroy(st);
+  delete s;
+}
+
 void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet shared)
   Slot* s = new Slot();
   HIPCHK(hipSetDevice(d->id));
-  HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&s->stream_msg, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&s->stream_pk, hipStreamNonBlocking));
-  s->set_stream(s->stream);
-  for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk, &s->join_mask})
-    HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
+  try {
+    HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&s->stream_msg, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&s->stream_pk, hipStreamNonBlocking));
+    s->set_stream(s->stream);
+    for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk, &s->join_mask})
+      HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
+  } catch (HipError&) {
+    free_slot(d, s);
+    throw;
+  }
   d->slots.push_back(s);
   d->workers.emplace_back(worker_loop, d, s);
+}
+
+// Brings the device to `want` slots: new slots start their dispatcher; surplus slots are retired (their dispatcher
+// finishes the run it holds, then exits) and freed.  Called with no device lock held.
+void resize_slots(Device* d, int64_t want) {
+  std::vector<std::thread> joins;
+  std::vector<Slot*> gone;
+  {
+    std::lock_guard<std::mutex> lk(d->q_mu);
+    while ((int64_t)d->slots.size() < want) add_slot(d);
+    while ((int64_t)d->slots.size() > want) {
+      Slot* s = d->slots.back();
+      s->retire = true;
+      gone.push_back(s);
+      joins.push_back(std::move(d->workers.back()));
+      d->slots.pop_back();
+      d->workers.pop_back();
+    }
+  }
+  d->q_cv.notify_all();
+  for (auto& t : joins) t.join();
+  for (Slot* s : gone) free_slot(d, s);
 }
 
 void destroy_device(Device* d) {
@@ -1082,24 +1360,37 @@ void destroy_device(Device* d) {
   }
   d->q_cv.notify_all();
   for (auto& t : d->workers) t.join();
+  for (Slot* s : d->slots) free_slot(d, s);
   (void)hipSetDevice(d->id);
-  for (Slot* s : d->slots) {
-    for (hipStream_t st : {s->stream, s->stream_msg, s->stream_pk})
-      if (st) (void)hipStreamSynchronize(st);
-    s->release_all();
-    if (s->stream) (void)hipStreamSynchronize(s->stream);  // the stream-ordered frees
-    for (auto& e : s->ev)
-      if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk, s->join_mask})
-      if (e) (void)hipEventDestroy(e);
-    for (hipStream_t st : {s->stream, s->stream_msg, s->stream_pk})
-      if (st) (void)hipStreamDestroy(st);
-    delete s;
-  }
   d->helper.release_all();
   d->table.release();
   if (d->table_stream) (void)hipStreamDestroy(d->table_stream);
   delete d;
+}
+
+// Hardware queues HIP gives this process per device: GPU_MAX_HW_QUEUES as HIP read it at its initialization
+// (HIP's default is 4).  Read-only: the library never writes the environment.
+int64_t hw_queues_of_process() {
+  const char* v = getenv("GPU_MAX_HW_QUEUES");
+  const long q = v ? strtol(v, nullptr, 10) : 0;
+  return q > 0 ? q : 4;
+}
+
+// Default slots per device: a slot's three streams (+ the device's table stream) should not share in-order
+// hardware queues with another slot's, where a kernel would wait behind an unrelated run's.
+int64_t default_slots(int64_t hw_queues) { return std::max<int64_t>(1, (hw_queues - 1) / 3); }
+
+// Creates the devices' slots on the first call (so a "slots" value set after init is the count created).
+int ensure_slots(blsgpu_ctx* ctx) {
+  std::lock_guard<std::mutex> lk(ctx->slots_mu);
+  if (ctx->slots_started) return BLSGPU_OK;
+  try {
+    for (Device* d : ctx->devs) resize_slots(d, ctx->slots_per_device);
+  } catch (HipError&) {
+    return BLSGPU_DEVICE_ERROR;
+  }
+  ctx->slots_started = true;
+  return BLSGPU_OK;
 }
 
 // Shards a call over the devices and queues the shard tasks.
@@ -1145,9 +1436,6 @@ extern "C" {
 int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
   if (!out) return BLSGPU_ERR_ARGS;
   *out = nullptr;
-  // Concurrent calls use one slot (and HIP stream) each; streams that share an in-order hardware queue
-  // serialize.  HIP reads GPU_MAX_HW_QUEUES once, at its initialization: the launcher sets it (bench.py and
-  // the Node addon's loader set 8 before the first HIP call; DESIGN.md "Hardware queues").
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return BLSGPU_ERR_NO_DEVICE;
   std::vector<int> ids;
@@ -1160,6 +1448,8 @@ int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
     for (int i = 0; i < count; i++) ids.push_back(i);
   }
   blsgpu_ctx* ctx = new blsgpu_ctx();
+  ctx->hw_queues = hw_queues_of_process();
+  ctx->slots_per_device = default_slots(ctx->hw_queues);
   try {
     for (int id : ids) {
       Device* d = new Device();
@@ -1167,7 +1457,6 @@ int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
       ctx->devs.push_back(d);
       HIPCHK(hipSetDevice(id));
       HIPCHK(hipStreamCreateWithFlags(&d->table_stream, hipStreamNonBlocking));
-      for (int k = 0; k < ctx->slots_per_device; k++) add_slot(d);
     }
   } catch (HipError&) {
     blsgpu_destroy(ctx);
@@ -1262,16 +1551,15 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   std::string k(key);
   if (k == "slots") {
     if (value < 1 || value > 64) return BLSGPU_ERR_ARGS;
-    try {
-      for (Device* d : ctx->devs) {
-        std::lock_guard<std::mutex> lk(d->q_mu);
-        while ((int64_t)d->slots.size() < value) add_slot(d);
+    std::lock_guard<std::mutex> sk(ctx->slots_mu);
+    ctx->slots_per_device = value;
+    if (ctx->slots_started) {
+      try {
+        for (Device* d : ctx->devs) resize_slots(d, value);
+      } catch (HipError&) {
+        return BLSGPU_DEVICE_ERROR;
       }
-    } catch (HipError&) {
-      return BLSGPU_DEVICE_ERROR;
     }
-    std::lock_guard<std::mutex> lk(ctx->opt_mu);
-    ctx->slots_per_device = std::max<int64_t>(ctx->slots_per_device, value);
     return BLSGPU_OK;
   }
   std::lock_guard<std::mutex> lk(ctx->opt_mu);
@@ -1291,9 +1579,59 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "miller_k") {
     if (value < 0 || value > 64) return BLSGPU_ERR_ARGS;
     ctx->opt.miller_k = value;
+  } else if (k == "group_policy") {
+    if (value < 0 || value > 1) return BLSGPU_ERR_ARGS;
+    ctx->opt.group_policy = value;
   } else {
     return BLSGPU_ERR_ARGS;
   }
+  return BLSGPU_OK;
+}
+
+int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
+  if (!cctx || !key || !value) return BLSGPU_ERR_ARGS;
+  blsgpu_ctx* ctx = const_cast<blsgpu_ctx*>(cctx);
+  const std::string k(key);
+  if (k == "slots") {
+    std::lock_guard<std::mutex> sk(ctx->slots_mu);
+    if (ctx->slots_started && !ctx->devs.empty()) {
+      std::lock_guard<std::mutex> lk(ctx->devs[0]->q_mu);
+      *value = (int64_t)ctx->devs[0]->slots.size();
+    } else {
+      *value = ctx->slots_per_device;
+    }
+    return BLSGPU_OK;
+  }
+  if (k == "hw_queues") {
+    *value = ctx->hw_queues;
+    return BLSGPU_OK;
+  }
+  if (k == "abi_version") {
+    *value = BLSGPU_ABI_VERSION;
+    return BLSGPU_OK;
+  }
+  std::lock_guard<std::mutex> lk(ctx->opt_mu);
+  const Options& o = ctx->opt;
+  if (k == "group_sets") *value = o.group_sets;
+  else if (k == "profile") *value = o.profile;
+  else if (k == "max_devices") *value = o.max_devices;
+  else if (k == "dedupe") *value = o.dedupe;
+  else if (k == "merge_sets") *value = o.merge_sets;
+  else if (k == "miller_k") *value = o.miller_k;
+  else if (k == "group_policy") *value = o.group_policy;
+  else return BLSGPU_ERR_ARGS;
+  return BLSGPU_OK;
+}
+
+int blsgpu_chunkify(uint32_t len, uint32_t min_per_chunk, uint32_t* chunk_first, uint32_t* n_chunks) {
+  if (!chunk_first || !n_chunks || min_per_chunk == 0) return BLSGPU_ERR_ARGS;
+  const uint32_t per = chunk_size(len, min_per_chunk);
+  uint32_t c = 0;
+  if (len / min_per_chunk <= 1) chunk_first[c++] = 0;  // [arr], also for an empty arr
+  else
+    for (uint32_t i = 0; i < len; i += per) chunk_first[c++] = i;
+  chunk_first[c] = len;
+  *n_chunks = c;
   return BLSGPU_OK;
 }
 
@@ -1316,6 +1654,10 @@ int blsgpu_verify(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, bl
     if (stats) *stats = blsgpu_stats{};
     leave(ctx);
     return BLSGPU_OK;
+  }
+  if (int e = ensure_slots(ctx)) {
+    leave(ctx);
+    return e;
   }
   launch_call(ctx, &c);
   std::unique_lock<std::mutex> lk(c.m);
@@ -1371,6 +1713,12 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, bl
     c->shards.clear();
     finish_call(c);  // calls done(user, OK) and leaves
     return BLSGPU_OK;
+  }
+  if (int e = ensure_slots(ctx)) {
+    delete c->owned;
+    delete c;
+    leave(ctx);
+    return e;
   }
   launch_call(ctx, c);
   return BLSGPU_OK;

@@ -37,6 +37,8 @@ EXPORTED_SYMBOLS = [
     "blsgpu_key_validate",
     "blsgpu_signing_roots",
     "blsgpu_shard_jobs",
+    "blsgpu_get_option",
+    "blsgpu_chunkify",
 ]
 ROOT_OBJECT = 0
 ROOT_ATTESTATION_DATA = 1
@@ -71,6 +73,7 @@ class Stats(ctypes.Structure):
         ("pairing_units", ctypes.c_uint32),
         ("miller_chunks", ctypes.c_uint32),
         ("run_sets", ctypes.c_uint32),
+        ("run_calls", ctypes.c_uint32),
     ]
 
 
@@ -125,6 +128,8 @@ def load():
     lib.blsgpu_key_validate.argtypes = [vp, u32, vp, u32, u32, vp, vp]
     lib.blsgpu_signing_roots.argtypes = [vp, ctypes.c_int, u32, vp, u32, vp, u32, vp]
     lib.blsgpu_shard_jobs.argtypes = [vp, vp, u32, u32, vp]
+    lib.blsgpu_get_option.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
+    lib.blsgpu_chunkify.argtypes = [u32, u32, vp, vp]
     _lib = lib
     return lib
 
@@ -144,6 +149,17 @@ def shard_jobs(job_first_set, n_parts, set_pk_first=None):
     if rc != OK:
         raise ValueError(f"blsgpu_shard_jobs -> {code_name(rc)}")
     return [(int(out[k]), int(out[k + 1])) for k in range(n_parts)]
+
+
+def chunkify(length, min_per_chunk):
+    """chunkifyMaximizeChunkSize(range(length), min_per_chunk) (reference multithread/utils.ts:4-19) through the
+    C-ABI (blsgpu_chunkify, pure host code): list of index lists."""
+    out = np.zeros(length // max(min_per_chunk, 1) + 2, np.uint32)
+    nc = ctypes.c_uint32(0)
+    rc = load().blsgpu_chunkify(length, min_per_chunk, out.ctypes.data, ctypes.addressof(nc))
+    if rc != OK:
+        raise ValueError(f"blsgpu_chunkify -> {code_name(rc)}")
+    return [list(range(int(out[k]), int(out[k + 1]))) for k in range(nc.value)]
 
 
 def _u8(b):
@@ -226,6 +242,13 @@ class Context:
         rc = self._lib.blsgpu_set_option(self.h, key.encode(), int(value))
         if rc != OK:
             raise ValueError(f"blsgpu_set_option({key}) -> {code_name(rc)}")
+
+    def get_option(self, key: str) -> int:
+        v = ctypes.c_int64(0)
+        rc = self._lib.blsgpu_get_option(self.h, key.encode(), ctypes.byref(v))
+        if rc != OK:
+            raise ValueError(f"blsgpu_get_option({key}) -> {code_name(rc)}")
+        return v.value
 
     def upload_pubkeys(self, first_index: int, pk96: bytes):
         n = len(pk96) // 96

@@ -1312,6 +1312,21 @@ static uint32_t chunk_size(uint32_t len, uint32_t min) {
   return cc <= 1 ? len : (len + cc - 1) / cc;
 }
 
+/* chunkifyMaximizeChunkSize as index lists: chunk_first[0..*n_chunks] (the reference returns [arr] when
+ * floor(len / min) <= 1, an empty arr included) */
+int blscpu_chunkify(uint32_t len, uint32_t min, uint32_t* chunk_first, uint32_t* n_chunks) {
+  if (!min || !chunk_first || !n_chunks) return BLSGPU_ERR_ARGS;
+  uint32_t c = 0, per = chunk_size(len, min);
+  if (len / min <= 1) {
+    chunk_first[c++] = 0;
+  } else {
+    for (uint32_t i = 0; i < len; i += per) chunk_first[c++] = i;
+  }
+  chunk_first[c] = len;
+  *n_chunks = c;
+  return 0;
+}
+
 /* worker.ts verifyManySignatureSets over one request's jobs */
 static void do_request(void* vc, uint32_t r) {
   pool_ctx* c = (pool_ctx*)vc;

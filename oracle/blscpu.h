@@ -58,6 +58,9 @@ int blscpu_verify_jobs(const blsgpu_batch* b, const blscpu_table* table, int8_t*
                        blscpu_stats* stats);
 
 /* instrumentation: Fp multiplications (mul + sqr) executed by the calling thread since the last reset */
+/* chunkifyMaximizeChunkSize (multithread/utils.ts:4-19) as chunk start indices (chunk_first[*n_chunks] = len) */
+int blscpu_chunkify(uint32_t len, uint32_t min_per_chunk, uint32_t* chunk_first, uint32_t* n_chunks);
+
 void blscpu_count_reset(void);
 uint64_t blscpu_count_get(void);
 

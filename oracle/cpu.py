@@ -63,6 +63,7 @@ def load():
     lib.blscpu_aggregate_pubkeys.argtypes = [ctypes.POINTER(Batch), vp, vp, u32, vp, i32]
     lib.blscpu_verify_jobs.argtypes = [ctypes.POINTER(Batch), vp, vp, i32, ctypes.POINTER(Stats)]
     lib.blscpu_count_get.restype = ctypes.c_uint64
+    lib.blscpu_chunkify.argtypes = [u32, u32, vp, vp]
     _lib = lib
     return lib
 
@@ -198,6 +199,15 @@ def aggregate_pubkeys(table=None, out_len=96, threads=0, **batch):
     if rc:
         raise RuntimeError(f"blscpu_aggregate_pubkeys -> {rc}")
     return [out[out_len * i: out_len * (i + 1)].tobytes() for i in range(b.n_sets)], st[: b.n_sets]
+
+
+def chunkify(length, min_per_chunk):
+    """chunkifyMaximizeChunkSize(range(length), min_per_chunk) as the oracle applies it: list of index lists."""
+    out = np.zeros(length // max(min_per_chunk, 1) + 2, np.uint32)
+    nc = ctypes.c_uint32(0)
+    if load().blscpu_chunkify(length, min_per_chunk, out.ctypes.data, ctypes.addressof(nc)):
+        raise ValueError("blscpu_chunkify")
+    return [list(range(int(out[k]), int(out[k + 1]))) for k in range(nc.value)]
 
 
 def count_reset():

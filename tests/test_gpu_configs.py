@@ -1,13 +1,24 @@
-"""GPU parity at BASELINE.json's config sizes through size-independent properties (the CPU oracle is far too
-slow for 10^4 pairings): every valid set verifies, every set signed over the wrong message makes exactly its
-own job false (invalid-batch fallback), results do not depend on batching or on the random scalars, and a
-corrupted aggregate fails only its own job.  Workloads come from bench.py's generators."""
+"""GPU parity at BASELINE.json's configs C3, C4 (one rank's shard and the whole 32,768-set step) and C5, job for job
+against the C restatement of the reference pool (oracle/blscpu.c verify_jobs, pinned by tests/test_cpu_oracle.py)
+on ORACLE-signed inputs: the workloads come from bench.py's generators with every signature made by
+the oracle, and ~1% of the sets are corrupted in every way the reference distinguishes (oracle/corrupt.py).  Both
+grouping policies run: the default >= 1,024-set groups and the reference pool's jobs / requests / chunks
+(group_policy 1), whose batchRetries / batchSigsSuccess metrics must equal the oracle's."""
+import os
+
 import numpy as np
 import pytest
 
 import bench
+from oracle import corrupt, cpu
 
 pytestmark = pytest.mark.gpu
+
+THREADS = bench.host_cpus()["threads"]
+
+
+def oracle_sign(sks, msgs):
+    return cpu.sign(sks, msgs, threads=THREADS)
 
 
 @pytest.fixture(scope="module")
@@ -19,56 +30,110 @@ def ctx():
     c.close()
 
 
-def run(ctx, w, seed=bench.SEED, **over):
-    call = {k: v for k, v in w.items() if k not in ("expected", "pks_table") and not k.startswith("_")}
+def call_of(w, **over):
+    call = {k: v for k, v in w.items() if k != "expected" and not k.startswith("_")}
     call.update(over)
-    res, st = ctx.verify_raw(**call, seed=seed)
-    return res, st
+    return call
 
 
-def test_c5_mixed_one_percent_invalid(ctx):
-    w, n, desc, _ = bench.build_workload(ctx, "C5", 0)
-    assert desc["invalid_sets"] == 10
-    res, st = run(ctx, w)
-    assert np.array_equal(res, w["expected"])
-    assert st.batch_retries >= 1  # the failing groups went through the fallback
-    # independent of the batch scalars and of batching (non-batchable: each job its own group)
-    res2, _ = run(ctx, w, seed=12345)
-    assert np.array_equal(res2, w["expected"])
-    res3, _ = run(ctx, w, job_flags=np.zeros(len(w["expected"]), np.uint8))
-    assert np.array_equal(res3, w["expected"])
-    # a message variant of the bench's in-flight pool (new roots, re-signed): the same per-job answers
-    w1 = bench.message_variant(ctx, w, 3)
-    assert not np.array_equal(w1["msgs"], w["msgs"])
-    res4, _ = run(ctx, w1)
-    assert np.array_equal(res4, w["expected"])
+def corrupted(w, seed):
+    """The workload's sets re-signed by the oracle over fresh roots, ~1% corrupted (every class)."""
+    n = len(w["_mkey"])
+    msgs = [bench.msg_j(k, seed) for k in w["_mkey"]]
+    sigs = cpu.sign(b"".join(w["_sk"]), b"".join(msgs), threads=THREADS)
+    msgs, buf, sl, applied = corrupt.corrupt_sets([sigs[96 * i: 96 * i + 96] for i in range(n)], msgs,
+                                                  np.random.default_rng(seed & 0xFFFF))
+    return call_of(w, sigs=np.frombuffer(buf, np.uint8), sig_len=np.asarray(sl, np.uint32),
+                   msgs=np.frombuffer(b"".join(msgs), np.uint8), sig_stride=192), applied
 
 
-def test_c3_block_import_aggregates(ctx):
-    w, n, desc, k = bench.build_workload(ctx, "C3", 0)
+def compare(ctx, call, table, seed=bench.SEED, policy=0):
+    ctx.set_option("group_policy", policy)
+    try:
+        got, st = ctx.verify_raw(**call, seed=seed)
+    finally:
+        ctx.set_option("group_policy", 0)
+    want, ost = cpu.verify_jobs(table=table, threads=THREADS, **call, seed=seed)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} mismatches, first {bad[:8]}: got {got[bad[:8]]} want {want[bad[:8]]}"
+    if policy == 1:  # the reference pool's metric units
+        assert (st.batch_retries, st.batch_sigs_success) == (ost.batch_retries, ost.batch_sigs_success)
+    return got, st
+
+
+def test_c5_mixed_vs_oracle(ctx):
+    w, n, desc, _ = bench.build_workload(ctx, "C5", 0, signer=oracle_sign)
+    assert desc["invalid_sets"] == 10 and n == 1024
+    table = bench.oracle_table(w)
+    got, st = compare(ctx, call_of(w), table)
+    assert np.array_equal(got, w["expected"]) and st.batch_retries >= 1
+    compare(ctx, call_of(w), table, policy=1)
+    compare(ctx, call_of(w), table, seed=12345)
+    compare(ctx, call_of(w, job_flags=np.zeros(len(w["expected"]), np.uint8)), table)  # every job its own group
+    bad, applied = corrupted(w, 0xC5)
+    got, _ = compare(ctx, bad, table)
+    assert len(set(got.tolist())) >= 5
+    compare(ctx, bad, table, policy=1)
+
+
+def test_c3_block_import_vs_oracle(ctx):
+    w, n, desc, k = bench.build_workload(ctx, "C3", 0, signer=oracle_sign)
     assert n == 128 and k == 512
-    res, _ = run(ctx, w)
-    assert list(res) == [1]
-    # as 128 separate jobs, then with one pubkey index of set 77 swapped (wrong aggregate -> only job 77 false)
+    table = bench.oracle_table(w)
+    got, _ = compare(ctx, call_of(w), table)
+    assert list(got) == [1]
+    # as 128 separate batchable jobs, then with one pubkey index of set 77 swapped (only job 77 false)
     jfs = np.arange(n + 1, dtype=np.uint32)
-    res, _ = run(ctx, w, job_first_set=jfs, job_flags=np.ones(n, np.uint8))
-    assert (res == 1).all()
+    got, _ = compare(ctx, call_of(w, job_first_set=jfs, job_flags=np.ones(n, np.uint8)), table)
+    assert (got == 1).all()
     pk = w["pk_index"].copy()
     pk[77 * 512 + 5] = 65535 - pk[77 * 512 + 5]
-    res, _ = run(ctx, w, job_first_set=jfs, job_flags=np.ones(n, np.uint8), pk_index=pk)
+    got, _ = compare(ctx, call_of(w, job_first_set=jfs, job_flags=np.ones(n, np.uint8), pk_index=pk), table)
     want = np.ones(n, np.int8)
     want[77] = 0
-    assert np.array_equal(res, want)
+    assert np.array_equal(got, want)
+    bad, _ = corrupted(w, 0xC3)
+    compare(ctx, dict(bad, job_first_set=jfs, job_flags=np.ones(n, np.uint8)), table)
+    compare(ctx, dict(bad, job_first_set=jfs, job_flags=np.ones(n, np.uint8)), table, policy=1)
 
 
-def test_c4_shard_of_epoch(ctx):
-    """One rank's shard of C4 (world 8): 4,096 aggregate sets over the 2^20-validator table."""
-    w, n, desc, _ = bench.build_workload(ctx, "C4", 0, 8)
-    assert n == 4096 and desc["total_sets_per_step"] == 32768
+@pytest.mark.parametrize("world", [8, 1])
+def test_c4_epoch_vs_oracle(ctx, world):
+    """world 8: one rank's shard (4,096 aggregate sets); world 1: the whole 32,768-set step on one device.  The
+    pubkeys come from the 2^20-validator device table."""
+    w, n, desc, _ = bench.build_workload(ctx, "C4", 0, world, signer=oracle_sign)
+    assert n == 32768 // world and desc["total_sets_per_step"] == 32768
     assert ctx.pubkeys_count >= 1 << 20
-    res, st = run(ctx, w)
-    assert (res == 1).all() and st.batch_retries == 0
-    sigs = w["sigs"].copy()
-    sigs[96 * 1000 : 96 * 1001] = w["sigs"][96 * 1001 : 96 * 1002]  # set 1001's sig on set 1000 (same committee)
-    res, _ = run(ctx, w, sigs=sigs)
-    assert list(np.nonzero(res != 1)[0]) == [1000] and res[1000] == 0
+    table = bench.oracle_table(w)
+    got, st = compare(ctx, call_of(w), table)
+    assert (got == 1).all() and st.batch_retries == 0
+    if world == 8:
+        sigs = w["sigs"].copy()
+        sigs[96 * 1000: 96 * 1001] = w["sigs"][96 * 1001: 96 * 1002]  # set 1001's sig on set 1000 (same committee)
+        got, _ = compare(ctx, call_of(w, sigs=sigs), table)
+        assert list(np.nonzero(got != 1)[0]) == [1000] and got[1000] == 0
+        bad, _ = corrupted(w, 0xC4)
+        compare(ctx, bad, table)
+        compare(ctx, bad, table, policy=1)
+
+
+def test_pool_policy_split_calls_vs_oracle(ctx):
+    """group_policy 1 on calls that the pool splits (> 128 sets: chunkify(sets, 128)) mixed with small batchable and
+    non-batchable calls and an empty call: per-call answers and the pool's metric units equal the oracle's."""
+    rng = np.random.default_rng(77)
+    sizes = [300, 1, 2, 129, 0, 64, 1, 1, 513, 7, 3, 128, 1, 40]
+    flags = [1, 1, 0, 1, 1, 0, 1, 0, 1, 1, 1, 0, 1, 1]
+    n = sum(sizes)
+    sks = [bench.interop_sk(i).to_bytes(32, "big") for i in range(n)]
+    msgs = [bench.msg_j(j, 0x9001) for j in range(n)]
+    sigs = oracle_sign(b"".join(sks), b"".join(msgs))
+    pks = cpu.sk_to_pk(b"".join(sks), threads=THREADS)
+    m2, buf, sl, _ = corrupt.corrupt_sets([sigs[96 * i: 96 * i + 96] for i in range(n)], msgs, rng, frac=0.004)
+    call = dict(job_first_set=np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32), sigs=buf, sig_len=sl,
+                msgs=b"".join(m2), pk_bytes=pks, job_flags=np.asarray(flags, np.uint8), sig_stride=192)
+    got, st = compare(ctx, call, None, policy=1)
+    assert got[4] == -10  # the empty call: "Empty signature set"
+    compare(ctx, call, None, policy=0)
+    clean = dict(call, sigs=sigs, sig_len=[96] * n, msgs=b"".join(msgs), sig_stride=96)
+    got, st = compare(ctx, clean, None, policy=1)
+    assert (np.delete(got, 4) == 1).all() and st.batch_retries == 0

@@ -362,3 +362,51 @@ def test_msm_exceptional_buckets_vs_oracle(ctx):
               pk_bytes=b"".join(pks[96 * i: 96 * i + 96] for i in idx[:-1]), job_flags=np.ones(n - 1))
     got, st = ctx.verify_raw(**ok)
     assert (got == 1).all() and st.batch_retries == 0
+
+
+def test_merged_run_isolates_bad_call():
+    """A call whose table index is beyond the device's table, queued between valid calls that a slot merges into one
+    pipeline run, fails alone (ERR_ARGS) and never joins the run; the valid calls of the run keep their own answers
+    (a bad call must not fail the calls merged with it)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from lodestar_amd.native import Context
+
+    n = 2048
+    rng = np.random.default_rng(21)
+    sks, pks, msgs, sigs, sig_len = corrupted_single_sets(n, b"merge", rng)
+    c = Context([0])
+    try:
+        c.set_option("slots", 1)
+        c.set_option("merge_sets", 1 << 20)
+        c.upload_pubkeys(0, pks)
+        assert c.get_option("slots") == 1
+        good = dict(job_first_set=np.arange(n + 1), sigs=sigs, sig_len=sig_len, msgs=b"".join(msgs),
+                    set_pk_first=np.arange(n + 1), pk_index=np.arange(n), job_flags=np.ones(n), sig_stride=192)
+        bad_idx = np.arange(n)
+        bad_idx[17] = n + 5  # beyond the 2048-entry table
+        bad = dict(good, pk_index=bad_idx)
+        want, _ = cpu.verify_jobs(table=cpu.Table(pks), threads=THREADS, **good)
+        with ThreadPoolExecutor(8) as pool:
+            futs = [pool.submit(c.verify_raw, **(bad if i in (2, 5) else good)) for i in range(8)]
+            outs = []
+            for i, f in enumerate(futs):
+                try:
+                    outs.append(f.result())
+                except RuntimeError as e:
+                    outs.append(e)
+        for i, o in enumerate(outs):
+            if i in (2, 5):
+                assert isinstance(o, RuntimeError) and "ERR_ARGS" in str(o)
+            else:
+                assert np.array_equal(o[0], want), i
+        assert max(o[1].run_calls for i, o in enumerate(outs) if i not in (2, 5)) >= 2  # some calls were merged
+        # slots resize both ways and report the count in use
+        c.set_option("slots", 3)
+        assert c.get_option("slots") == 3
+        c.set_option("slots", 2)
+        assert c.get_option("slots") == 2
+        got, _ = c.verify_raw(**good)
+        assert np.array_equal(got, want)
+    finally:
+        c.close()
