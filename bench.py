@@ -455,6 +455,9 @@ def main():
                     help="runtime slots per GPU (0 = the runtime's default for the process's hardware queues); fewer "
                          "slots than calls in flight make each slot merge the queued calls into one pipeline run")
     ap.add_argument("--merge-sets", type=int, default=131072, help="max sets of one merged pipeline run (0 = never)")
+    ap.add_argument("--pipeline-depth", type=int, default=None, help="runs in flight per device (runtime default 2)")
+    ap.add_argument("--merge-wait-us", type=int, default=None,
+                    help="how long a slot lingers for more calls to merge while runs are in flight (runtime default)")
     ap.add_argument("--miller-k", type=int, default=0,
                     help="pairings per Miller accumulator (shared squarings); 0 = the runtime's choice by run size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -487,6 +490,10 @@ def main():
         ctx.set_option("slots", args.slots)
     ctx.set_option("merge_sets", args.merge_sets)
     ctx.set_option("miller_k", args.miller_k)
+    if args.pipeline_depth is not None:
+        ctx.set_option("pipeline_depth", args.pipeline_depth)
+    if args.merge_wait_us is not None:
+        ctx.set_option("merge_wait_us", args.merge_wait_us)
     work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev)
     expected = work.pop("expected", None)
     if expected is None:
@@ -532,10 +539,12 @@ def main():
     barrier()
     sync()
     t0 = time.perf_counter()
+    w0 = time.monotonic_ns()  # the timed window on CLOCK_MONOTONIC, the clock of rocprofv3's kernel timestamps
     results = list(pool.map(step, range(args.steps)))
     sync()
     barrier()
     dt = time.perf_counter() - t0
+    w1 = time.monotonic_ns()
     ctx.set_option("profile", 0)
     stats = [r[0] for r in results]
     call_lat = np.array([r[1] for r in results])
@@ -571,7 +580,8 @@ def main():
         "config": dict(desc, group_sets=args.group_sets, group_policy=args.group_policy,
                        batch_groups_per_step=groups, inflight=args.inflight,
                        slots=ctx.get_option("slots"), hw_queues=ctx.get_option("hw_queues"),
-                       merge_sets=args.merge_sets, pipeline_runs_timed=len(runs_timed),
+                       merge_sets=args.merge_sets, pipeline_depth=ctx.get_option("pipeline_depth"),
+                       merge_wait_us=ctx.get_option("merge_wait_us"), pipeline_runs_timed=len(runs_timed),
                        parallelism=f"shard-by-job x{n_gpus} ({'one process per GPU' if world > 1 else 'in-process devices'}), no collective"),
         "p50_batch_latency_ms": round(float(np.median(lat)), 3),
         "call_latency_under_load_ms": {"p50": round(float(np.percentile(call_lat, 50)), 2),
@@ -596,6 +606,7 @@ def main():
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(call, expected, table, hc)
     out["workload_variants"] = {"count": n_var, "gen_s": round(t_gen, 2)}
+    out["timed_window_monotonic_ns"] = [w0, w1]  # tools/occupancy.py --window: the timed steps' kernels in a trace
     if rank == 0:
         print(json.dumps(out), flush=True)
     pool.shutdown()

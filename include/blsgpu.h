@@ -142,10 +142,13 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
 /* Tunables: "group_sets" (sets per batch group before a new one opens, default 1024), "slots" (runtime slots
  * per device, 1..64; default by hardware queues), "max_devices" (devices one call may shard over, default all),
  * "dedupe" (message dedupe + same-message pairing, 0/1, default 1), "miller_k" (pairings per Miller
- * accumulator sharing its Fp12 squarings, 1..64; default 0 = by run size: 1 below 32768 sets, 2 below 65536,
- * else 4), "merge_sets" (a runtime slot merges calls
+ * accumulator sharing its Fp12 squarings, 1..64; default 0 = by run size: 1 below 131072 pairings, 2 below
+ * 262144, else 4), "merge_sets" (a runtime slot merges calls
  * already queued on its device into one pipeline run of up to this many sets -- jobs and results stay per
- * call -- default 65536, 0 = never), "profile" (per-stage kernel times in
+ * call -- default 131072, 0 = never), "pipeline_depth" (runs a device keeps in flight, default 2: its slots share
+ * the device's streams, so a further run would only queue behind them), "merge_wait_us" (while runs are in
+ * flight, a slot forming a run waits up to this long for more calls to merge, default 2000; an idle device starts
+ * at once), "profile" (per-stage kernel times in
  * blsgpu_stats.stage_ms, 0/1), "group_policy" (0 = batch groups of >= group_sets sets, the default; 1 = the
  * reference pool's grouping: calls split into <= 128-set jobs (chunkifyMaximizeChunkSize(sets, 128),
  * multithread/index.ts:156), packed into >= 128-set worker requests (prepareWork, index.ts:386-401), each

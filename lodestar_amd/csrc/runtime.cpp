@@ -102,12 +102,11 @@ constexpr size_t kMillerLineWords = (size_t)MILLER_STEPS * W_LINE;
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// One in-flight shard on one device: a stream and every per-call buffer.
+// One runtime slot: a dispatcher's staging and work buffers and its events.  The HIP streams belong to the device
+// (Device::st) and are shared by its slots, so a device needs kStreams hardware queues whatever its slot count.
 struct Slot {
-  // Three streams per slot: the run's independent branches overlap -- signatures + the batch tail on `stream`,
-  // hash_to_G2 + Miller lines on `stream_msg`, pubkey aggregation + r_i pk_i on `stream_pk` -- joined by events.
-  hipStream_t stream = nullptr, stream_msg = nullptr, stream_pk = nullptr;
-  hipEvent_t join_in = nullptr, join_msg = nullptr, join_pk = nullptr, join_mask = nullptr;  // no timing
+  hipEvent_t join_in = nullptr, join_msg = nullptr, join_pk = nullptr, join_mask = nullptr, join_gsm = nullptr,
+             done = nullptr;  // no timing
   hipEvent_t ev[2 * (kStages + 2)] = {};  // profile: (start, end) per stage; pairs kStages, kStages + 1 = the
                                           // Miller lines, the groups' MillerLoop(-g1, S) (parts of stages 5, 7)
   // d_in / h_in: every per-call input packed into one arena (one H2D transfer); d_res / h_res: job errors +
@@ -116,8 +115,11 @@ struct Slot {
   DevBuf<uint32_t> d_work, d_lines, d_S, d_F, d_G, d_list, d_msmB, d_msmW, d_fb;
   HostBuf<uint8_t> h_in, h_res, h_ok;
   HostBuf<uint32_t> h_list;
-  bool retire = false;  // set under the device queue lock: the dispatcher exits instead of taking work
+  bool retire = false;     // set under the device queue lock: the dispatcher exits instead of taking work
+  bool in_flight = false;  // the slot's run counts in Device::runs_inflight
 
+  // the stream buffer growth is ordered on (hipFreeAsync / hipMallocAsync); the slot's previous work is complete
+  // whenever it grows a buffer (its dispatcher waits for each run), so only this ordering matters
   void set_stream(hipStream_t st) {
     for (auto* b : {&d_in, &d_res, &d_bytes, &d_ok}) b->st = st;
     for (auto* b : {&d_work, &d_lines, &d_S, &d_F, &d_G, &d_list, &d_msmB, &d_msmW, &d_fb}) b->st = st;
@@ -136,9 +138,15 @@ struct Task {
   uint32_t shard;
 };
 
+// The device's pipeline streams, shared by its slots: one per branch of a run's DAG (run_shard).  Runs of different
+// slots queue behind each other per branch, so the chip always has the next run's work while one run's tail drains.
+enum { kSig = 0, kMsg = 1, kPk = 2, kTail = 3, kStreams = 4 };
+
 struct Device {
   int id = 0;
   hipStream_t table_stream = nullptr;  // uploads and the synchronous helpers (debug, aggregate, ...)
+  hipStream_t st[kStreams] = {};
+  std::mutex enq_mu;  // one run's batch (or fallback) launches are enqueued without another slot's in between
   std::mutex helper_mu;
   Slot helper;  // buffers of the synchronous helpers (on table_stream)
   // pubkey table (AoS, W_PKTAB words per key): verification holds it shared, uploads exclusive
@@ -152,6 +160,7 @@ struct Device {
   bool stop = false;
   std::vector<Slot*> slots;
   std::vector<std::thread> workers;
+  int runs_inflight = 0;  // under q_mu: runs taken by a slot whose batch pass has not completed
 };
 
 inline uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
@@ -169,7 +178,9 @@ struct Options {  // snapshot taken at the start of each call
   bool profile = false;
   bool dedupe = true;
   int64_t miller_k = 0;  // pairings per Miller accumulator (shared squarings); 0 = by run size (miller_k_auto)
-  int64_t merge_sets = 65536;  // queued calls a slot merges into one pipeline run (sets), 0 = never
+  int64_t merge_sets = 131072;  // queued calls a slot merges into one pipeline run (sets), 0 = never
+  int64_t merge_wait_us = 2000;  // while runs are in flight, a slot waits this long for more calls to merge
+  int64_t pipeline_depth = 2;    // runs a device has in flight (taken by a slot, batch pass not yet complete)
   int64_t group_policy = 0;    // 0 = groups of >= group_sets sets; 1 = the reference pool's jobs / requests / chunks
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
@@ -192,11 +203,13 @@ struct GroupPlanEntry {
 };
 
 // Pairings per Miller accumulator when the option is 0: shared squarings save work (k = 4: 3,483 products per
-// pairing vs 5,162 at k = 1, lodestar_amd/op_counts.json) but leave n / k lanes; keep >= 16384 lanes (256 waves)
-// so an isolated call still spreads over the chip, and use k = 4 for merged runs.
+// pairing vs 5,162 at k = 1, lodestar_amd/op_counts.json) but leave n / k lanes.  The accumulation is one wave per
+// SIMD, so k doubles only while n / 2k still gives every SIMD a wave (>= 65,536 lanes = 1,024 waves): below that
+// the stage would hold fewer SIMDs for longer on the run's critical path (r03c trace: k = 2 at 54k sets held 341
+// waves for 14 ms).
 inline uint32_t miller_k_auto(uint32_t n_items) {
   uint32_t k = 1;
-  while (k < 4 && n_items / (2 * k) >= 16384) k *= 2;
+  while (k < 4 && n_items / (2 * k) >= 65536) k *= 2;
   return k;
 }
 
@@ -337,6 +350,18 @@ struct MsgIndex {
 };
 
 // Runs one device's shard on one slot.  Writes job_result[job_begin..job_end).
+// A slot's run leaves the device's in-flight count (once): its batch pass is complete on the GPU, so another slot
+// may start the next run while this one finishes on the host (results, fallback round trips).
+void release_inflight(Device& d, Slot& sl) {
+  {
+    std::lock_guard<std::mutex> lk(d.q_mu);
+    if (!sl.in_flight) return;
+    sl.in_flight = false;
+    d.runs_inflight--;
+  }
+  d.q_cv.notify_all();
+}
+
 // With `plan` (group_policy 1), the groups are the plan's job ranges instead of >= group_sets packing, and the
 // batchRetries / batchSigsSuccess metrics count the plan's batchable chunks the way the worker does (worker.ts:
 // 56-84: a chunk that throws or returns false is one retry; a chunk that verifies adds all its sets).
@@ -499,6 +524,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   else
     in_bytes = o_pk + (size_t)n * 96;
   const size_t o_pk2 = al256(o_pk + (size_t)(n + 1) * 4);
+  sl.set_stream(d.st[kSig]);  // buffer growth of the batch pass, ordered before the input copy on the same stream
   sl.h_in.ensure(in_bytes);
   sl.d_in.ensure(in_bytes);
   uint8_t* const hin = sl.h_in.p;
@@ -563,9 +589,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   const size_t per_set = W_G2A + W_G1J + W_G1A + W_FP12 + 8 * W_G1J + 2 * W_FP + (merged ? W_G1A : 0);
   sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * (W_G2A + W_G2J + W_FP + 14 * W_FP + 2 * W_G2J));
   sl.d_lines.ensure((size_t)nm * kMillerLineWords);
-  hipStream_t s = sl.stream;
+  hipStream_t s = d.st[kSig];
   uint8_t* const din = sl.d_in.p;
-  HIPCHK(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, s));
   uint8_t* const d_ok0 = sl.d_res.p + o_ok;
 
   PipelineBuffers pb;
@@ -623,77 +648,86 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.job_err = reinterpret_cast<int8_t*>(sl.d_res.p);
 
   // ---- kernel pipeline ------------------------------------------------------------------------------------
-  // DAG of one run on three streams after the input copy:
-  //   signatures: decode -> [pubkeys done] job mask -> MSM -> MillerLoop(-g1, S_g) -> [Miller F done] final exp.
-  //   messages:   hash_to_G2 -> affine -> Miller lines -> [job mask done] Miller accumulation -> F reduction
-  //   pubkeys:    aggregate -> r_i pk_i -> affine
-  // An isolated call's critical path drops from the sum of the stages to the longer of the branches plus the final
-  // exponentiation; a full chip just interleaves the branches.
+  // DAG of one run on the device's four streams (shared by its slots: the next run of another slot queues behind
+  // this one per branch, so the chip has its work while this run's tail drains):
+  //   signatures (kSig): input copy -> decode -> [pubkeys done] job mask -> MSM -> MillerLoop(-g1, S_g)
+  //   messages (kMsg):   hash_to_G2 -> affine -> Miller lines -> [job mask done] Miller accumulation -> F reduction
+  //   pubkeys (kPk):     aggregate -> r_i pk_i -> affine
+  //   tail (kTail):      [S_g Miller + F done] final exponentiation per group -> results copy
+  // An isolated call's critical path is the longer of the branches plus the final exponentiation.
   const bool prof = opt.profile;
-  hipStream_t sm = sl.stream_msg, sp = sl.stream_pk;
+  hipStream_t sm = d.st[kMsg], sp = d.st[kPk], stl = d.st[kTail];
   auto beg = [&](int k, hipStream_t st) {
     if (prof) HIPCHK(hipEventRecord(sl.ev[2 * k], st));
   };
   auto end = [&](int k, hipStream_t st) {
     if (prof) HIPCHK(hipEventRecord(sl.ev[2 * k + 1], st));
   };
-  HIPCHK(hipEventRecord(sl.join_in, s));
-  HIPCHK(hipStreamWaitEvent(sm, sl.join_in, 0));
-  HIPCHK(hipStreamWaitEvent(sp, sl.join_in, 0));
-  // messages
-  beg(1, sm);
-  launch_hash_to_g2(pb, sm);
-  launch_h_affine(pb, sm);
-  end(1, sm);
-  beg(kStages, sm);
-  if (!coop) launch_miller_lines(pb, sm);
-  end(kStages, sm);
-  // pubkeys
-  beg(2, sp);
-  if ((table_mode || bytes_agg) && pb.n_agg) launch_pk_aggregate(pb, n, sp);
-  end(2, sp);
-  beg(3, sp);
-  launch_pk_finish(pb, n, sp);
-  launch_pk_affine(pb, n, sp);
-  end(3, sp);
-  HIPCHK(hipEventRecord(sl.join_pk, sp));
-  // signatures, then the batch equation
-  beg(0, s);
-  launch_sig_decode(pb, n, s);
-  end(0, s);
-  HIPCHK(hipStreamWaitEvent(s, sl.join_pk, 0));
-  beg(4, s);
-  launch_job_mask(pb, s);
-  HIPCHK(hipEventRecord(sl.join_mask, s));
-  // the message branch continues with the Miller accumulation once the include mask exists
-  HIPCHK(hipStreamWaitEvent(sm, sl.join_mask, 0));
-  beg(5, sm);
-  if (merged) launch_unit_aggregate(pb, sm);
-  if (coop)
-    launch_miller_coop(pb, merged, sm);
-  else
-    launch_miller_acc(pb, merged, sm);
-  end(5, sm);
-  const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
-  beg(6, sm);
-  launch_group_reduce(pb, d_franges, ng0, sl.d_F.p, sm);
-  end(6, sm);
-  HIPCHK(hipEventRecord(sl.join_msg, sm));
-  const uint32_t* d_slices = reinterpret_cast<uint32_t*>(din + o_slices);
-  const uint32_t* d_rslices = reinterpret_cast<uint32_t*>(din + o_rslices);
-  launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s);
-  end(4, s);
-  // MillerLoop(-g1, S_g) of every group now, while the message branch still runs
-  beg(kStages + 1, s);
-  launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, s);
-  end(kStages + 1, s);
-  HIPCHK(hipStreamWaitEvent(s, sl.join_msg, 0));
-  beg(7, s);
-  launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, s, nullptr, 0, sl.d_G.p);
-  end(7, s);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(sl.h_res.p, sl.d_res.p, o_ok + ng0, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  {
+    std::lock_guard<std::mutex> enq(d.enq_mu);
+    HIPCHK(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(sl.join_in, s));
+    HIPCHK(hipStreamWaitEvent(sm, sl.join_in, 0));
+    HIPCHK(hipStreamWaitEvent(sp, sl.join_in, 0));
+    // messages
+    beg(1, sm);
+    launch_hash_to_g2(pb, sm);
+    launch_h_affine(pb, sm);
+    end(1, sm);
+    beg(kStages, sm);
+    if (!coop) launch_miller_lines(pb, sm);
+    end(kStages, sm);
+    // pubkeys
+    beg(2, sp);
+    if ((table_mode || bytes_agg) && pb.n_agg) launch_pk_aggregate(pb, n, sp);
+    end(2, sp);
+    beg(3, sp);
+    launch_pk_finish(pb, n, sp);
+    launch_pk_affine(pb, n, sp);
+    end(3, sp);
+    HIPCHK(hipEventRecord(sl.join_pk, sp));
+    // signatures, then the batch equation
+    beg(0, s);
+    launch_sig_decode(pb, n, s);
+    end(0, s);
+    HIPCHK(hipStreamWaitEvent(s, sl.join_pk, 0));
+    beg(4, s);
+    launch_job_mask(pb, s);
+    HIPCHK(hipEventRecord(sl.join_mask, s));
+    // the message branch continues with the Miller accumulation once the include mask exists
+    HIPCHK(hipStreamWaitEvent(sm, sl.join_mask, 0));
+    beg(5, sm);
+    if (merged) launch_unit_aggregate(pb, sm);
+    if (coop)
+      launch_miller_coop(pb, merged, sm);
+    else
+      launch_miller_acc(pb, merged, sm);
+    end(5, sm);
+    const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
+    beg(6, sm);
+    launch_group_reduce(pb, d_franges, ng0, sl.d_F.p, sm);
+    end(6, sm);
+    HIPCHK(hipEventRecord(sl.join_msg, sm));
+    const uint32_t* d_slices = reinterpret_cast<uint32_t*>(din + o_slices);
+    const uint32_t* d_rslices = reinterpret_cast<uint32_t*>(din + o_rslices);
+    launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s);
+    end(4, s);
+    // MillerLoop(-g1, S_g) of every group now, while the message branch still runs
+    beg(kStages + 1, s);
+    launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, s);
+    end(kStages + 1, s);
+    HIPCHK(hipEventRecord(sl.join_gsm, s));
+    HIPCHK(hipStreamWaitEvent(stl, sl.join_gsm, 0));
+    HIPCHK(hipStreamWaitEvent(stl, sl.join_msg, 0));
+    beg(7, stl);
+    launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, stl, nullptr, 0, sl.d_G.p);
+    end(7, stl);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(sl.h_res.p, sl.d_res.p, o_ok + ng0, hipMemcpyDeviceToHost, stl));
+    HIPCHK(hipEventRecord(sl.done, stl));
+  }
+  HIPCHK(hipEventSynchronize(sl.done));
+  release_inflight(d, sl);
   st.groups += ng0;
   st.unique_messages += n_umsg;
   st.pairing_units += merged ? n_units : n;
@@ -773,6 +807,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     // 8-12 KB/lane of scratch, which the per-queue scratch reservation does not always get.
     constexpr uint32_t kFbLaneMin = 128;
     const uint32_t nr = (uint32_t)retry.size();
+    sl.set_stream(stl);  // the fallback runs on the tail stream, its buffers grow there
     std::vector<uint32_t> rfirst{0}, ritems, rr(2 * (size_t)nr), rf(2 * (size_t)nr), rsl, rrs{0}, rset;
     for (uint32_t q = 0; q < nr; q++) {
       const auto js = job_sets(retry[q]);
@@ -815,38 +850,39 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     uint32_t* const dF = sl.d_F.p;
     uint32_t* const dS_sub = sl.d_S.p + (size_t)W_G2J * nr;
     uint32_t* const dF_sub = sl.d_F.p + (size_t)W_FP12 * nr;
-    HIPCHK(hipMemcpyAsync(sl.d_list.p, hl, o_sel * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(sl.d_list.p, hl, o_sel * 4, hipMemcpyHostToDevice, stl));
     PipelineBuffers pr = pb;
     pr.n_chunks = nc;
     pr.chunk_first = sl.d_list.p + 4 * (size_t)nr;
     pr.chunk_items = sl.d_list.p + 4 * (size_t)nr + rfirst.size();
     if (coop)  // no stored lines in a cooperative run: the per-job chunks hold one set each (mk = 1)
-      launch_miller_coop(pr, false, s);
+      launch_miller_coop(pr, false, stl);
     else
-      launch_miller_acc(pr, false, s);
+      launch_miller_acc(pr, false, stl);
     if (small_jobs) {
       // r_i sig_i for the retried sets (G2 window tables and results in the fallback's own buffers)
       sl.d_fb.ensure((size_t)stride * 9 * W_G2J);
       pr.rsig = sl.d_fb.p;
       pr.scal_tab = sl.d_fb.p + (size_t)stride * W_G2J;
-      launch_sig_scale(pr, (uint32_t)rset.size(), s, sl.d_list.p + o_rset);
-      launch_group_reduce_lane(pr, sl.d_list.p, sl.d_list.p + 2 * (size_t)nr, nr, dS, dF, s);
+      launch_sig_scale(pr, (uint32_t)rset.size(), stl, sl.d_list.p + o_rset);
+      launch_group_reduce_lane(pr, sl.d_list.p, sl.d_list.p + 2 * (size_t)nr, nr, dS, dF, stl);
     } else {
       sl.d_msmB.ensure((size_t)MSM_BUCKET_WORDS * std::max<uint32_t>(nrs, 1));
       sl.d_msmW.ensure((size_t)MSM_WINDOW_WORDS * nr);
-      launch_sig_msm(pr, sl.d_list.p + o_rsl, nrs, sl.d_list.p + o_rrs, nr, sl.d_msmB.p, sl.d_msmW.p, dS, s);
-      launch_group_reduce(pr, sl.d_list.p + 2 * (size_t)nr, nr, dF, s);
+      launch_sig_msm(pr, sl.d_list.p + o_rsl, nrs, sl.d_list.p + o_rrs, nr, sl.d_msmB.p, sl.d_msmW.p, dS, stl);
+      launch_group_reduce(pr, sl.d_list.p + 2 * (size_t)nr, nr, dF, stl);
     }
     std::vector<uint32_t> sel;  // jobs to check on their own
     if (nsub) {
       if (nsub >= kFbLaneMin)
-        launch_range_combine_lane(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, s);
+        launch_range_combine_lane(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, stl);
       else
-        launch_range_combine(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, s);
-      launch_group_check(dS_sub, dF_sub, nsub, sl.d_ok.p + nr, s);
+        launch_range_combine(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, stl);
+      launch_group_check(dS_sub, dF_sub, nsub, sl.d_ok.p + nr, stl);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(sl.h_ok.p + nr, sl.d_ok.p + nr, nsub, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipMemcpyAsync(sl.h_ok.p + nr, sl.d_ok.p + nr, nsub, hipMemcpyDeviceToHost, stl));
+      HIPCHK(hipEventRecord(sl.done, stl));
+      HIPCHK(hipEventSynchronize(sl.done));
       for (uint32_t t = 0; t < nsub; t++)
         for (uint32_t q = subr[2 * t]; q < subr[2 * t + 1]; q++) {
           if (sl.h_ok.p[nr + t]) jr[retry[q]] = 1;
@@ -858,11 +894,12 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     if (!sel.empty()) {
       const uint32_t ns = (uint32_t)sel.size();
       memcpy(hl + o_sel, sel.data(), (size_t)ns * 4);
-      HIPCHK(hipMemcpyAsync(sl.d_list.p + o_sel, hl + o_sel, (size_t)ns * 4, hipMemcpyHostToDevice, s));
-      launch_group_check(dS, dF, nr, sl.d_ok.p, s, sl.d_list.p + o_sel, ns);
+      HIPCHK(hipMemcpyAsync(sl.d_list.p + o_sel, hl + o_sel, (size_t)ns * 4, hipMemcpyHostToDevice, stl));
+      launch_group_check(dS, dF, nr, sl.d_ok.p, stl, sl.d_list.p + o_sel, ns);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, ns, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, ns, hipMemcpyDeviceToHost, stl));
+      HIPCHK(hipEventRecord(sl.done, stl));
+      HIPCHK(hipEventSynchronize(sl.done));
       for (uint32_t k = 0; k < ns; k++) jr[retry[sel[k]]] = sl.h_ok.p[k] ? 1 : 0;
     }
   }
@@ -1254,25 +1291,45 @@ void worker_loop(Device* d, Slot* sl) {
     std::vector<Task> parts;
     {
       std::unique_lock<std::mutex> lk(d->q_mu);
-      d->q_cv.wait(lk, [&] { return d->stop || sl->retire || !d->queue.empty(); });
+      // Run formation.  A device keeps at most pipeline_depth runs in flight (the streams are shared, so a further
+      // run would only queue behind them); a free slot takes the oldest queued call and merges the compatible calls
+      // queued behind it, up to merge_sets sets.  While other runs are in flight the GPU is busy anyway, so the
+      // slot lingers up to merge_wait_us for more calls to merge: bursts of calls become a few chip-filling runs
+      // instead of many small ones; an idle device starts at once (an isolated call pays no wait).
+      d->q_cv.wait(lk, [&] {
+        return d->stop || sl->retire ||
+               (!d->queue.empty() && d->runs_inflight < std::max<int64_t>(1, d->queue.front().call->opt.pipeline_depth));
+      });
       if (sl->retire) return;
       if (d->queue.empty()) return;  // stop requested and nothing left
       parts.push_back(d->queue.front());
       d->queue.pop_front();
-      // merge further queued shards of compatible calls, up to merge_sets sets in total
       const Call* c0 = parts[0].call;
       uint32_t total = task_sets(parts[0]);
       const int64_t cap = c0->opt.merge_sets;
-      while (!d->queue.empty() && cap > 0 && !(c0->ctx->closed)) {
-        const Task& nx = d->queue.front();
-        const Call* c = nx.call;
-        if ((int64_t)(total + task_sets(nx)) > cap || pk_mode(c->b) != pk_mode(c0->b) || !c->opt.same_run(c0->opt))
-          break;
-        total += task_sets(nx);
-        parts.push_back(nx);
-        d->queue.pop_front();
+      const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(c0->opt.merge_wait_us);
+      for (;;) {
+        while (!d->queue.empty() && cap > 0 && !(c0->ctx->closed)) {
+          const Task& nx = d->queue.front();
+          const Call* c = nx.call;
+          if ((int64_t)(total + task_sets(nx)) > cap || pk_mode(c->b) != pk_mode(c0->b) || !c->opt.same_run(c0->opt))
+            break;
+          total += task_sets(nx);
+          parts.push_back(nx);
+          d->queue.pop_front();
+        }
+        const bool room = cap > 0 && (int64_t)total < cap && d->queue.empty();
+        if (!room || d->runs_inflight == 0 || d->stop || c0->ctx->closed) break;
+        if (d->q_cv.wait_until(lk, deadline) == std::cv_status::timeout && d->queue.empty()) break;
       }
+      d->runs_inflight++;
+      sl->in_flight = true;
     }
+    struct InflightGuard {  // the run leaves the in-flight count when its batch pass completes (run_shard) or here
+      Device* d;
+      Slot* sl;
+      ~InflightGuard() { release_inflight(*d, *sl); }
+    } guard{d, sl};
     if (parts.size() == 1) {
       run_task(*d, *sl, parts[0]);
       continue;
@@ -1296,19 +1353,17 @@ void worker_loop(Device* d, Slot* sl) {
   }
 }
 
-// Frees a slot whose dispatcher has exited (or never started).
+// Frees a slot whose dispatcher has exited (or never started): its buffers (stream-ordered frees on the stream the
+// slot last grew them on, then that stream is drained) and events.
 void free_slot(Device* d, Slot* s) {
   (void)hipSetDevice(d->id);
-  for (hipStream_t st : {s->stream, s->stream_msg, s->stream_pk})
-    if (st) (void)hipStreamSynchronize(st);
+  hipStream_t last = s->d_in.st;
   s->release_all();
-  if (s->stream) (void)hipStreamSynchronize(s->stream);  // the stream-ordered frees
+  if (last) (void)hipStreamSynchronize(last);
   for (auto& e : s->ev)
     if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk, s->join_mask})
+  for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk, s->join_mask, s->join_gsm, s->done})
     if (e) (void)hipEventDestroy(e);
-  for (hipStream_t st : {s->stream, s->stream_msg, s->stream_pk})
-    if (st) (void)hipStreamDestroy(st);
   delete s;
 }
 
@@ -1316,11 +1371,8 @@ void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet sh
   Slot* s = new Slot();
   HIPCHK(hipSetDevice(d->id));
   try {
-    HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&s->stream_msg, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&s->stream_pk, hipStreamNonBlocking));
-    s->set_stream(s->stream);
-    for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk, &s->join_mask})
+    s->set_stream(d->st[kSig]);
+    for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk, &s->join_mask, &s->join_gsm, &s->done})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
   } catch (HipError&) {
@@ -1362,6 +1414,8 @@ void destroy_device(Device* d) {
   for (auto& t : d->workers) t.join();
   for (Slot* s : d->slots) free_slot(d, s);
   (void)hipSetDevice(d->id);
+  for (hipStream_t st : d->st)
+    if (st) (void)hipStreamSynchronize(st), (void)hipStreamDestroy(st);
   d->helper.release_all();
   d->table.release();
   if (d->table_stream) (void)hipStreamDestroy(d->table_stream);
@@ -1376,9 +1430,10 @@ int64_t hw_queues_of_process() {
   return q > 0 ? q : 4;
 }
 
-// Default slots per device: a slot's three streams (+ the device's table stream) should not share in-order
-// hardware queues with another slot's, where a kernel would wait behind an unrelated run's.
-int64_t default_slots(int64_t hw_queues) { return std::max<int64_t>(1, (hw_queues - 1) / 3); }
+// Default slots per device.  Slots share the device's kStreams streams, so the count no longer depends on the
+// hardware queues; several slots let one run's host work (merging, packing, fallback round trips) overlap another's
+// kernels.
+int64_t default_slots(int64_t) { return 3; }
 
 // Creates the devices' slots on the first call (so a "slots" value set after init is the count created).
 int ensure_slots(blsgpu_ctx* ctx) {
@@ -1413,7 +1468,7 @@ void launch_call(blsgpu_ctx* ctx, Call* c) {
       std::lock_guard<std::mutex> lk(d->q_mu);
       d->queue.push_back({c, k});
     }
-    d->q_cv.notify_one();
+    d->q_cv.notify_all();  // a lingering slot (merge_wait_us) must see it, not only an idle one
   }
 }
 
@@ -1457,6 +1512,7 @@ int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
       ctx->devs.push_back(d);
       HIPCHK(hipSetDevice(id));
       HIPCHK(hipStreamCreateWithFlags(&d->table_stream, hipStreamNonBlocking));
+      for (hipStream_t& st : d->st) HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     }
   } catch (HipError&) {
     blsgpu_destroy(ctx);
@@ -1582,6 +1638,12 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "group_policy") {
     if (value < 0 || value > 1) return BLSGPU_ERR_ARGS;
     ctx->opt.group_policy = value;
+  } else if (k == "merge_wait_us") {
+    if (value < 0 || value > 1000000) return BLSGPU_ERR_ARGS;
+    ctx->opt.merge_wait_us = value;
+  } else if (k == "pipeline_depth") {
+    if (value < 1 || value > 64) return BLSGPU_ERR_ARGS;
+    ctx->opt.pipeline_depth = value;
   } else {
     return BLSGPU_ERR_ARGS;
   }
@@ -1619,6 +1681,8 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "merge_sets") *value = o.merge_sets;
   else if (k == "miller_k") *value = o.miller_k;
   else if (k == "group_policy") *value = o.group_policy;
+  else if (k == "merge_wait_us") *value = o.merge_wait_us;
+  else if (k == "pipeline_depth") *value = o.pipeline_depth;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }

@@ -42,9 +42,9 @@
  */
 const path = require("path");
 
-// Concurrent submissions run on separate runtime slots (HIP streams); HIP reads the hardware-queue count once,
-// at its first call (blsgpu_init), so the loader sets it unless the launcher already did (DESIGN.md).
-if (!process.env.GPU_MAX_HW_QUEUES) process.env.GPU_MAX_HW_QUEUES = "8";
+// CommonJS implementation (.cjs, so it stays CommonJS inside the "type": "module" beacon-node package); ESM callers
+// import it through index.js, TypeScript through index.d.ts.  The module never writes process.env: the runtime sizes
+// its slots to the hardware queues HIP gives the process (include/blsgpu.h blsgpu_init).
 const addon = require(path.join(__dirname, "blsgpu_napi.node"));
 
 const MAX_BUFFERED_SIGS = 32; // multithread/index.ts:48
@@ -73,12 +73,14 @@ function jobError(code) {
 
 class BlsGpuVerifier {
   /**
-   * @param {{devices?: number[], groupSets?: number, seed?: number}} opts
+   * @param {{devices?: number[], groupSets?: number, groupPolicy?: number, seed?: number}} opts
    * @param {{metrics?: object, logger?: object}} modules
    */
   constructor(opts = {}, modules = {}) {
     this.ctx = addon.init(opts.devices || null);
     if (opts.groupSets) addon.setOption(this.ctx, "group_sets", opts.groupSets);
+    // 1 = the pool's job / request / chunk structure (batchRetries / batchSigsSuccess in the reference's units)
+    if (opts.groupPolicy) addon.setOption(this.ctx, "group_policy", opts.groupPolicy);
     this.seed = opts.seed || 0; // 0 = OS CSPRNG batch scalars; fixed only for comparison runs
     this.metrics = modules.metrics || null;
     this.closed = false;
@@ -104,6 +106,11 @@ class BlsGpuVerifier {
 
   get deviceCount() {
     return addon.deviceCount(this.ctx);
+  }
+
+  /** A runtime tunable or property (include/blsgpu.h blsgpu_get_option: "slots", "hw_queues", "group_sets", ...). */
+  getOption(key) {
+    return addon.getOption(this.ctx, key);
   }
 
   /**

@@ -214,6 +214,23 @@ static napi_value SetOption(napi_env env, napi_callback_info info) {
   return NULL;
 }
 
+static napi_value GetOption(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  CtxBox* box = get_open_box(env, argv[0]);
+  if (!box) return NULL;
+  char key[64];
+  size_t kl;
+  CHECK(env, napi_get_value_string_utf8(env, argv[1], key, sizeof key, &kl));
+  int64_t value = 0;
+  int rc = blsgpu_get_option(box->ctx, key, &value);
+  if (rc != BLSGPU_OK) return throw_code(env, "getOption", rc);
+  napi_value out;
+  CHECK(env, napi_create_int64(env, value, &out));
+  return out;
+}
+
 static napi_value CodeName(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
@@ -405,6 +422,7 @@ static napi_value ModuleInit(napi_env env, napi_value exports) {
       {"uploadPubkeys", NULL, UploadPubkeys, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"pubkeysCount", NULL, PubkeysCount, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"setOption", NULL, SetOption, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"getOption", NULL, GetOption, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"codeName", NULL, CodeName, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"submit", NULL, Submit, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"keyValidate", NULL, KeyValidate, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},

@@ -1,5 +1,5 @@
 "use strict";
-// GPU parity of the JS drop-in (lodestar_amd/node/BlsGpuVerifier.js) against tests/golden/verify_sets.json,
+// GPU parity of the JS drop-in (lodestar_amd/node/BlsGpuVerifier.cjs) against tests/golden/verify_sets.json,
 // mirroring the reference's packages/beacon-node/test/e2e/chain/bls/multithread.test.ts:
 //   - valid sets verify true (single and aggregate, batchable and not);
 //   - a wrong signature resolves false, a malformed one rejects with its BLST code, and neither affects
@@ -18,7 +18,7 @@ const {
   verifySignatureSet,
   fastAggregateVerify,
   ethFastAggregateVerify,
-} = require(path.join(ROOT, "lodestar_amd", "node", "BlsGpuVerifier.js"));
+} = require(path.join(ROOT, "lodestar_amd", "node", "BlsGpuVerifier.cjs"));
 const fx = JSON.parse(fs.readFileSync(path.join(ROOT, "tests", "golden", "verify_sets.json"), "utf8"));
 const fav = JSON.parse(fs.readFileSync(path.join(ROOT, "tests", "golden", "fav_cases.json"), "utf8"));
 

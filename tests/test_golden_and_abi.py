@@ -85,10 +85,26 @@ def test_node_addon_loads_and_exports():
         "let threw = null; try { new m.BlsGpuVerifier(); } catch (e) { threw = e.message; }"
         "console.log(JSON.stringify({threw}));"
     )
-    out = subprocess.run([NODE, "-e", script, os.path.join(ROOT, "lodestar_amd", "node", "BlsGpuVerifier.js")],
+    out = subprocess.run([NODE, "-e", script, os.path.join(ROOT, "lodestar_amd", "node", "BlsGpuVerifier.cjs")],
                          capture_output=True, text=True, timeout=60)
     assert out.returncode == 0, out.stderr
     import torch
 
     if not torch.cuda.is_available():
         assert "NO_DEVICE" in json.loads(out.stdout)["threw"]
+
+
+@pytest.mark.skipif(NODE is None or not os.path.exists(ADDON), reason="node or the N-API addon is absent")
+def test_esm_entry_imports():
+    """The ES-module entry (lodestar_amd/node/index.js, package.json "type": "module" like the reference's
+    packages/beacon-node/package.json:15) imports the CommonJS implementation through createRequire and exposes the
+    IBlsVerifier surface; without a GPU the constructor fails loudly."""
+    out = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "esm_entry.mjs")], capture_output=True, text=True,
+                         timeout=60)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["esm"] and {"BlsGpuVerifier", "BlsGpuSingleThreadVerifier", "verifySignatureSet"} <= set(r["exports"])
+    import torch
+
+    if not torch.cuda.is_available():
+        assert "NO_DEVICE" in r["threw"]
