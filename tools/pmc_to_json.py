@@ -32,7 +32,7 @@ def main(prefix, out):
                    "WRITE_SIZE_kB_per_launch": round(w.get(k, (0, 0))[0], 1),
                    "launches": f.get(k, (0, 0))[1]} for k in sorted(set(f) | set(w))}
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, kernel trace only), "
-                     "bench.py --steps 4 --warmup 1 --inflight 1 --slots 1 --no-profile (C2, 16384 sets per launch)",
+                     "bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-parity --no-profile (the driver command; C2, merged runs)",
            "units": "kB per launch as reported; gfx950 FETCH_SIZE counts 1/2 of wide streaming reads "
                     "(MI355X_MICROARCH.md HBM section) -> bytes = 2 x 1024 x FETCH_SIZE; WRITE_SIZE exact",
            "kernels": kernels}
