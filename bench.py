@@ -313,26 +313,28 @@ def roofline(runs, n_sets, group_count, pubkeys_per_set, sets_per_s, miller_k=2,
     return out
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
-PMC_SETS_PER_LAUNCH = 16384  # the C2 launch the counters were collected on (tools/gpurun/r02_pmc.sh)
+PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
+# grid work-items per distinct message (C2: one message per set) of the hash stage's launches; k_batch_inv runs one
+# lane per INV_K = 16 elements (csrc/k_inv.hip), k_hash_map two lanes per message (one SSWU map each)
+PMC_ITEMS_PER_UNIT = {"k_hash_map": 2.0, "k_batch_inv": 1.0 / 16}
 
 
 def pmc_traffic(kernel, n_sets):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (FETCH_SIZE doubled for the
-    gfx950 half-count of wide reads, WRITE_SIZE as is; MI355X_MICROARCH.md HBM section), collected on
-    16,384-set launches and scaled linearly to an n_sets launch (every stage is lane-per-set, so its traffic --
-    inputs, outputs, scratch -- is per set); None when no PMC file is committed."""
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes over the driver's own command
+    (tools/gpurun/r03_e.sh; FETCH_SIZE doubled for the gfx950 half-count of wide reads, WRITE_SIZE as is;
+    MI355X_MICROARCH.md HBM section), kept as bytes per grid work-item because the merged runs differ in size, and
+    multiplied by the work-items of an n_sets launch; None when no PMC file is committed."""
     if not n_sets or not os.path.exists(PMC_FILE):
         return None
     with open(PMC_FILE) as fh:
         table = json.load(fh)["kernels"]
     # a stage is several launches ("k_a+k_b+..."); k_batch_inv's figure is per launch of either of its two uses
     parts = kernel.split("+")
-    if not all(p in table for p in parts):
+    if not all(p in table and "FETCH_B_per_item" in table[p] for p in parts):
         return None
-    b16k = sum(2 * 1024 * table[p]["FETCH_SIZE_kB_per_launch"] + 1024 * table[p]["WRITE_SIZE_kB_per_launch"]
-               for p in parts)
-    return round(b16k * n_sets / PMC_SETS_PER_LAUNCH)
+    per_unit = sum((table[p]["FETCH_B_per_item"] + table[p]["WRITE_B_per_item"]) * PMC_ITEMS_PER_UNIT.get(p, 1.0)
+                   for p in parts)
+    return round(per_unit * n_sets)
 
 
 BLST_SETS_PER_CORE = 2200.0  # published anchor: ~0.9 ms/set/thread, x2 batched (BASELINE.md)

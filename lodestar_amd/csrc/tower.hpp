@@ -106,9 +106,9 @@ BLS_INL fp2 fp2_sqr_body(const fp2& a) {
 #if defined(__HIP_DEVICE_COMPILE__) && !BLS_INLINE_PRODUCTS && !BLS_FP2_CLASSIC
 #define BLS_FP2_LDS_LANES 128
 __shared__ uint32_t bls_fp2_arg[2 * BLS_NL * BLS_FP2_LDS_LANES];
-struct fp2_ret {
-  uint32_t l[2 * BLS_NL];
-};
+// The 28-dword result comes back in VGPRs as a 32-wide vector: clang's AMDGPU ABI returns an aggregate of more than
+// 16 dwords indirectly (through a scratch sret slot: 7 dwordx4 stores + 7 loads per call), a vector type directly.
+typedef uint32_t fp2_ret __attribute__((ext_vector_type(32)));
 __device__ __noinline__ fp2_ret fp2_mul_r(BLS_PARAMS14(a), BLS_PARAMS14(c)) {
   const fp x0 = BLS_INIT14(a), x1 = BLS_INIT14(c);
   const uint32_t t = threadIdx.x;
@@ -122,8 +122,8 @@ __device__ __noinline__ fp2_ret fp2_mul_r(BLS_PARAMS14(a), BLS_PARAMS14(c)) {
   fp2_ret o;
 #pragma unroll
   for (int i = 0; i < BLS_NL; i++) {
-    o.l[i] = r.c0.l[i];
-    o.l[BLS_NL + i] = r.c1.l[i];
+    o[i] = r.c0.l[i];
+    o[BLS_NL + i] = r.c1.l[i];
   }
   return o;
 }
@@ -132,8 +132,8 @@ __device__ __noinline__ fp2_ret fp2_sqr_r(BLS_PARAMS14(a), BLS_PARAMS14(c)) {
   fp2_ret o;
 #pragma unroll
   for (int i = 0; i < BLS_NL; i++) {
-    o.l[i] = r.c0.l[i];
-    o.l[BLS_NL + i] = r.c1.l[i];
+    o[i] = r.c0.l[i];
+    o[BLS_NL + i] = r.c1.l[i];
   }
   return o;
 }
@@ -141,8 +141,8 @@ __device__ __forceinline__ fp2 fp2_from_ret(const fp2_ret& o) {
   fp2 r;
 #pragma unroll
   for (int i = 0; i < BLS_NL; i++) {
-    r.c0.l[i] = o.l[i];
-    r.c1.l[i] = o.l[BLS_NL + i];
+    r.c0.l[i] = o[i];
+    r.c1.l[i] = o[BLS_NL + i];
   }
   return r;
 }
@@ -167,8 +167,8 @@ __device__ __noinline__ fp2_ret fp2_mul_fp_r(BLS_PARAMS14(a), BLS_PARAMS14(c)) {
   fp2_ret o;
 #pragma unroll
   for (int i = 0; i < BLS_NL; i++) {
-    o.l[i] = r0.l[i];
-    o.l[BLS_NL + i] = r1.l[i];
+    o[i] = r0.l[i];
+    o[BLS_NL + i] = r1.l[i];
   }
   return o;
 }
