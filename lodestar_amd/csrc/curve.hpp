@@ -164,6 +164,31 @@ BLS_HDNI jac<F> jac_mul_zabs(const jac<F>& P) {
   return r;
 }
 
+// The same chain with P re-read through `loadP` at each of the five additions (|z| has Hamming weight 6), so the
+// doubling loop carries only the accumulator across the product calls; holding P in registers too made the
+// compiler spill it around every call.  The kernels keep P in their SoA buffers (k_hash.hip, k_sig.hip).
+template <class F, class LoadP>
+BLS_INL jac<F> jac_mul_zabs_ld(LoadP loadP) {
+  jac<F> r = loadP();
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    r = jac_dbl(r);
+    if ((BLS_Z_ABS >> i) & 1ull) r = jac_add(r, loadP());
+  }
+  return r;
+}
+// affine P (never infinity): mixed additions
+template <class F, class LoadA>
+BLS_INL jac<F> jac_mul_zabs_lda(LoadA loadA) {
+  jac<F> r = jac_from_aff(loadA());
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    r = jac_dbl(r);
+    if ((BLS_Z_ABS >> i) & 1ull) r = jac_add_aff(r, loadA());
+  }
+  return r;
+}
+
 BLS_HDNI bool jac_to_aff(const g1j& p, g1a& out) {
   if (jac_is_inf(p)) return false;
   fp zi = fp_inv(p.z);
@@ -214,6 +239,12 @@ BLS_HDNI bool g2_in_subgroup(const g2a& p) {
   g2j P = jac_from_aff(p);
   g2j zP = jac_neg(jac_mul_zabs(P));
   return jac_eq(g2_psi(P), zP);
+}
+// the same check with the affine P read through `loadA` (k_sig_decode: from its output buffer)
+template <class LoadA>
+BLS_INL bool g2_in_subgroup_ld(LoadA loadA) {
+  const g2j zP = jac_neg(jac_mul_zabs_lda<fp2>(loadA));
+  return jac_eq(g2_psi(jac_from_aff(loadA())), zP);
 }
 
 BLS_HD bool g1_on_curve(const g1a& p) {

@@ -390,8 +390,10 @@ BLS_HDNI fp fp_pow_words(const fp& a, const uint32_t* e, int nbits) {
     uint32_t d = 0;
     for (int k = i; k >= j; k--) d = (d << 1) | ((e[k >> 5] >> (k & 31)) & 1u);
     if (started) {
+      // the table entry is read before the window's squarings, so its (scratch) load latency hides behind them
+      const fp t = tab[d >> 1];
       for (int k = i; k >= j; k--) r = BLS_POW_SQR(r);
-      r = BLS_POW_MUL(r, tab[d >> 1]);
+      r = BLS_POW_MUL(r, t);
     } else {
       r = tab[d >> 1];
       started = true;

@@ -231,6 +231,24 @@ BLS_HDNI g2j clear_cofactor_g2(const g2j& P) {
   return jac_add(t3, jac_neg(P));
 }
 
+// clear_cofactor_g2 with its intermediate points in three caller-provided slots (SoA memory in k_hash_clear)
+// instead of registers, reordered so that only the accumulator is live across each [|z|] chain:
+//   A = [|z|]P,   C = psi^2(2P) - psi(P) + A - P,   D = [|z|](A - psi(P)),   h_eff P = C + D
+// (clear_cofactor_g2's t3 + t2 - t1 - P with t1 = -A, t2 = D, t3 = psi^2(2P) - psi(P)).  Slot 0 holds P on entry;
+// slots 1 and 2 are overwritten.
+template <class Ld, class St>
+BLS_INL g2j clear_cofactor_g2_slots(Ld ld, St st) {
+  const g2j A = jac_mul_zabs_ld<fp2>([&] { return ld(0); });
+  {
+    const g2j P = ld(0);
+    const g2j psiP = g2_psi(P);
+    st(1, jac_add(A, jac_neg(psiP)));
+    st(2, jac_add(jac_add(g2_psi2(jac_dbl(P)), jac_neg(psiP)), jac_add(A, jac_neg(P))));
+  }
+  const g2j D = jac_mul_zabs_ld<fp2>([&] { return ld(1); });
+  return jac_add(D, ld(2));
+}
+
 // hash_to_G2 in two halves around the one inversion of the two maps, so a kernel can batch that inversion over
 // many messages (k_hash.hip + k_inv.hip):
 //   prep:   u0, u1 = hash_to_field(msg); Zu2_j = Z u_j^2; tv_j = Zu2_j^2 + Zu2_j; d = a0 a1 (a_j = tv_j, or 1

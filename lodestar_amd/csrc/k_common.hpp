@@ -40,6 +40,14 @@
 #define BLSGPU_WPE_HMAP BLSGPU_WPE_HASH
 #endif
 
+// x, hidden from the optimizer: an SoA load whose lane index goes through this is recomputed where it is issued.
+// Inside a loop (the five additions of a [|z|] chain) the compiler otherwise hoists the point's 84 loop-invariant
+// 64-bit addresses out of the loop and spills them to scratch around the product calls.
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 __device__ __forceinline__ fp ld_fp(const uint32_t* p, uint32_t n, uint32_t i, int w0) {
   fp r;
 #pragma unroll

@@ -12,12 +12,19 @@ STAGE_KERNEL_W(BLSGPU_WPE_DEC) void k_sig_decode(PipelineBuffers b, uint32_t n_s
   for (uint32_t k = 0; k < cl; k++) raw[k] = src[k];
   g2a p;
   bool inf = false;
-  int st = sig_decode(raw, len, p, inf);
+  int st = sig_decode_point(raw, len, p, inf);
   if (st != BLS_OK || inf) {
     p.x = fp2_zero();
     p.y = fp2_zero();
   }
   st_g2a(b.sig_aff, b.n, i, p);
+  // subgroup check with P re-read from the output buffer (curve.hpp jac_mul_zabs_ld: no P across the chain)
+  if (st == BLS_OK && !inf && !g2_in_subgroup_ld([&] { return ld_g2a(b.sig_aff, b.n, opaque_u32(i)); })) {
+    st = BLS_POINT_NOT_IN_GROUP;
+    p.x = fp2_zero();
+    p.y = fp2_zero();
+    st_g2a(b.sig_aff, b.n, i, p);
+  }
   b.flags[i] = inf ? SF_SIG_INF : 0;  // sig flags: flags[0, n)
   b.status[i] = (int8_t)st;
 }

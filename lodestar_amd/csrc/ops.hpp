@@ -27,9 +27,9 @@ BLS_HD bool bytes_all_zero(const uint8_t* b, int n) {
 }
 
 // Deserialize a G2 signature: 96-byte compressed or 192-byte uncompressed (blst_p2_deserialize /
-// POINTonE2_Uncompress_Z semantics), then subgroup-check it (`validate = true`, maybeBatch.ts:23,36).
+// POINTonE2_Uncompress_Z semantics) -- everything of Signature.fromBytes but the subgroup check.
 // Returns a status; on success `inf` tells whether the point is the identity.
-BLS_HDNI int sig_decode(const uint8_t* b, uint32_t len, g2a& out, bool& inf) {
+BLS_HDNI int sig_decode_point(const uint8_t* b, uint32_t len, g2a& out, bool& inf) {
   inf = false;
   if (len != 96 && len != 192) return BLS_INVALID_SIZE;
   const uint8_t b0 = b[0];
@@ -71,8 +71,13 @@ BLS_HDNI int sig_decode(const uint8_t* b, uint32_t len, g2a& out, bool& inf) {
     if (!g2_on_curve(p)) return BLS_POINT_NOT_ON_CURVE;
     out = p;
   }
-  if (!g2_in_subgroup(out)) return BLS_POINT_NOT_IN_GROUP;
   return BLS_OK;
+}
+// ... then subgroup-check it (`validate = true`, maybeBatch.ts:23,36)
+BLS_HDNI int sig_decode(const uint8_t* b, uint32_t len, g2a& out, bool& inf) {
+  const int st = sig_decode_point(b, len, out, inf);
+  if (st != BLS_OK || inf) return st;
+  return g2_in_subgroup(out) ? BLS_OK : BLS_POINT_NOT_IN_GROUP;
 }
 
 // Deserialize a trusted 96-byte uncompressed affine G1 public key (blst_p1_deserialize semantics,

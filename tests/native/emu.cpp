@@ -261,6 +261,11 @@ int emu_hash_to_g2(const uint8_t* msg, uint8_t* out192) {
   return 1;
 }
 int emu_g2_in_subgroup(const uint8_t* p192) { return g2_in_subgroup(load_g2(p192)); }
+// the kernel's form (k_sig.hip): P re-read from memory along the chain
+int emu_g2_in_subgroup_ld(const uint8_t* p192) {
+  const g2a p = load_g2(p192);
+  return g2_in_subgroup_ld([&] { return p; });
+}
 int emu_g2_mul_u64(const uint8_t* p192, uint64_t k, uint8_t* out192) {
   g2a a;
   if (!jac_to_aff(jac_mul_u64(load_g2(p192), k), a)) return 0;
@@ -323,9 +328,11 @@ extern "C" int emu_hash_to_g2_split(const uint8_t* msg, uint8_t* out192) {
   h2c_prep h;
   hash_to_g2_prep(msg, h);
   const fp2 dinv = fp2_inv(h.d);
-  const g2j Q = jac_add(hash_to_g2_map_j(h, dinv, 0), hash_to_g2_map_j(h, dinv, 1));
+  g2j slot[3];
+  slot[0] = jac_add(hash_to_g2_map_j(h, dinv, 0), hash_to_g2_map_j(h, dinv, 1));
+  const g2j H = clear_cofactor_g2_slots([&](int k) { return slot[k]; }, [&](int k, const g2j& v) { slot[k] = v; });
   g2a a;
-  if (!jac_to_aff(clear_cofactor_g2(Q), a)) return 0;
+  if (!jac_to_aff(H, a)) return 0;
   g2a_to_be192(a, out192);
   return 1;
 }

@@ -113,6 +113,7 @@ def test_subgroup_and_scalar_mul():
     o = buf(192)
     Q = bls.g2_mul(bls.G2_GEN, 987654321)
     assert L.emu_g2_in_subgroup(g2b(Q)) == 1
+    assert L.emu_g2_in_subgroup_ld(g2b(Q)) == 1
     # random non-subgroup point
     while True:
         x = (rnd.randrange(P), rnd.randrange(P))
@@ -120,6 +121,7 @@ def test_subgroup_and_scalar_mul():
         if y:
             break
     assert L.emu_g2_in_subgroup(g2b((x, y))) == 0
+    assert L.emu_g2_in_subgroup_ld(g2b((x, y))) == 0
     for k in [1, 2, 3, 0xFFFFFFFFFFFFFFFF, rnd.getrandbits(64)]:
         assert L.emu_g2_mul_u64(g2b(Q), k, o) == 1
         assert b2g2(o.raw) == bls.g2_mul(Q, k)
