@@ -1556,9 +1556,10 @@ int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* 
     std::shared_lock<std::shared_mutex> lk(d->table_mu);
     if (first_index > d->table_n) result = BLSGPU_ERR_ARGS;
   }
-  try {
-    for (Device* d : ctx->devs) {
-      if (result) break;
+  // every device decodes and stores its own replica; the devices upload concurrently (one host thread each), so a
+  // 2^20-key table on 8 GPUs costs one device's upload time, not eight
+  auto upload_one = [&](Device* d) -> int {
+    try {
       HIPCHK(hipSetDevice(d->id));
       hipStream_t ts = d->table_stream;
       const uint32_t need = first_index + n;
@@ -1593,10 +1594,24 @@ int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* 
       (void)hipFree(dpk);
       (void)hipFree(dst);
       (void)hipFree(tmp);
-      if (err) result = err;
+      return err;
+    } catch (HipError&) {
+      return BLSGPU_DEVICE_ERROR;
+    } catch (std::exception&) {
+      return BLSGPU_DEVICE_ERROR;
     }
-  } catch (HipError&) {
-    result = BLSGPU_DEVICE_ERROR;
+  };
+  if (!result) {
+    std::vector<int> rc(ctx->devs.size(), 0);
+    if (ctx->devs.size() == 1) {
+      rc[0] = upload_one(ctx->devs[0]);
+    } else {
+      std::vector<std::thread> th;
+      for (size_t k = 0; k < ctx->devs.size(); k++) th.emplace_back([&, k] { rc[k] = upload_one(ctx->devs[k]); });
+      for (auto& t : th) t.join();
+    }
+    for (int r : rc)
+      if (r && !result) result = r;
   }
   leave(ctx);
   return result;

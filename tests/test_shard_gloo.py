@@ -93,3 +93,23 @@ def test_shard_gloo_world2():
     covered = sorted(j for a, b in ranges for j in range(a, b))
     assert covered == list(range(len(jfs) - 1))  # each job exactly once
     assert all(r[2] == 1.5 for r in res)  # max over ranks
+
+
+def test_c4_in_process_shard_ranges():
+    """bench.py --gpus N --config C4 (in-process): ONE call of the 32,768 aggregate sets of C4 (one batchable job
+    per set, committees of 512 with 0-10% dropout), which the runtime splits over the N devices with
+    blsgpu_shard_jobs -- strong scaling.  The ranges tile the call, match the rank rule, and give every device
+    its 1/N of the sets (the sets cost alike)."""
+    from lodestar_amd.native import shard_jobs as cpp_shard
+
+    rng = np.random.default_rng(0x4C4F444553544152)
+    n_sets = 2048 * 16
+    pks = np.array([512 - int(512 * rng.random() * 0.10 * rng.random()) for _ in range(n_sets)])
+    jfs = np.arange(n_sets + 1, dtype=np.uint32)
+    spf = np.concatenate([[0], np.cumsum(pks)]).astype(np.uint32)
+    for n in (1, 2, 4, 8):
+        sh = cpp_shard(jfs, n, spf)
+        assert sh == shard_jobs(jfs, n, spf)
+        assert sh[0][0] == 0 and sh[-1][1] == n_sets and all(a[1] == b[0] for a, b in zip(sh, sh[1:]))
+        sizes = [b - a for a, b in sh]
+        assert max(sizes) - min(sizes) <= max(64, n_sets // n // 50), sizes
