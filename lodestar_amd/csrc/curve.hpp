@@ -234,6 +234,16 @@ BLS_FN g2j g2_psi2(const g2j& p) {
   return r;
 }
 
+// The endomorphism with eigenvalue lambda = -z^2 (mod r) on both groups, for the batch scalars r = a + b lambda
+// (k_common.hpp jac_mul_scalar_word, msm.hpp): G1 phi(x, y) = (beta x, y) -- the map g1_in_subgroup checks as
+// -[z^2] -- and on G2 -psi^2 (psi = [z] there, so psi^2 = [z^2]).  Both act on Jacobian coordinates directly.
+BLS_FN g1j endo_lambda(const g1j& p) {
+  g1j r = p;
+  r.x = fp_mul(p.x, G1_BETA);
+  return r;
+}
+BLS_FN g2j endo_lambda(const g2j& p) { return jac_neg(g2_psi2(p)); }
+
 // P in G2  <=>  psi(P) == [z]P  (z = -|z|)   (Scott, eprint 2021/1130)
 BLS_HDNI bool g2_in_subgroup(const g2a& p) {
   g2j P = jac_from_aff(p);

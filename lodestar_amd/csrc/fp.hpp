@@ -404,7 +404,115 @@ BLS_HDNI fp fp_pow_words(const fp& a, const uint32_t* e, int nbits) {
 }
 #endif
 
-BLS_HD fp fp_inv(const fp& a) { return fp_pow_words(a, EXP_P_MINUS_2, 381); }   // 0 -> 0
+BLS_HD fp fp_inv_pow(const fp& a) { return fp_pow_words(a, EXP_P_MINUS_2, 381); }   // 0 -> 0
+
+// ------------------------------------------------------------------------------------------------
+// Inversion by Bernstein-Yang divsteps ("safegcd", eprint 2019/266): the extended binary gcd of p and the canonical
+// value x of the element, in batches of 28 divsteps whose 2x2 transition matrix is found from the low 32 bits of
+// f, g alone and then applied to the full-width f, g and to the Bezout coefficients d, e (kept mod p by adding the
+// multiple of p that makes each batch's division by 2^28 exact -- a one-limb Montgomery step).  The control flow
+// does not depend on the data (a fixed 40 batches: the paper's bound floor((49 * 381 + 57) / 17) = 1101 divsteps for
+// 381-bit inputs), so the 64 lanes of a wave stay converged.  ~40k 32-bit VALU operations against ~460 Montgomery
+// products (~210k instructions) for x^(p-2): an inversion on a latency-critical lane (the final exponentiation's,
+// the batched affine conversions') costs a tenth of the exponentiation.
+// Invariants: f = d x, g = e x (mod p); at the end g = 0 and f = +-1, so x^-1 = f d.  Multi-limb signed values: 14
+// limbs, 0..12 in [0, 2^28), limb 13 a signed int32 (two's-complement top).
+// ------------------------------------------------------------------------------------------------
+#define BLS_BY_BATCHES 40
+#define BLS_BY_STEPS 28
+
+// (u a + v b) / 2^28 (exact: the caller's low 28 bits vanish) and, with `modp`, plus m p for the m that makes them
+// vanish; a, b, out: signed 14-limb values (out may alias a or b)
+BLS_INL void by_lincomb(const int32_t* a, const int32_t* b, int32_t u, int32_t v, bool modp, int32_t* out) {
+  int64_t acc = (int64_t)u * a[0] + (int64_t)v * b[0];
+  int32_t m = 0;
+  if (modp) {
+    m = (int32_t)(((uint32_t)acc * BLS_N0INV) & BLS_MASK);
+    acc += (int64_t)m * (int64_t)FP_P.l[0];
+  }
+  acc >>= BLS_LB;  // the low 28 bits are zero
+  int32_t o[BLS_NL];
+#pragma unroll
+  for (int j = 1; j < BLS_NL; j++) {
+    acc += (int64_t)u * a[j] + (int64_t)v * b[j];
+    if (modp) acc += (int64_t)m * (int64_t)FP_P.l[j];
+    o[j - 1] = (int32_t)((uint32_t)acc & BLS_MASK);
+    acc >>= BLS_LB;
+  }
+  o[BLS_NL - 1] = (int32_t)acc;
+#pragma unroll
+  for (int j = 0; j < BLS_NL; j++) out[j] = o[j];
+}
+
+BLS_HDNI fp fp_inv(const fp& a) {  // 0 -> 0
+  const fp x = fp_canon(a);
+  int32_t F[BLS_NL], G[BLS_NL], D[BLS_NL], E[BLS_NL];
+#pragma unroll
+  for (int j = 0; j < BLS_NL; j++) {
+    F[j] = (int32_t)FP_P.l[j];
+    G[j] = (int32_t)x.l[j];
+    D[j] = 0;
+    E[j] = 0;
+  }
+  E[0] = 1;
+  int32_t delta = 1;
+#pragma unroll 1
+  for (int bt = 0; bt < BLS_BY_BATCHES; bt++) {
+    // low 32 bits of f and g (limb 0 + the low 4 bits of limb 1): exact enough for 28 divsteps
+    uint32_t f = (uint32_t)F[0] | ((uint32_t)F[1] << BLS_LB), g = (uint32_t)G[0] | ((uint32_t)G[1] << BLS_LB);
+    int32_t u = 1, v = 0, q = 0, r = 1;  // [f; g] 2^i = [u v; q r] [f0; g0] over the batch
+#pragma unroll
+    for (int i = 0; i < BLS_BY_STEPS; i++) {
+      // delta > 0 and g odd: (f, g, row f, row g) <- (g, -f, row g, -row f), delta <- -delta
+      const bool sw = delta > 0 && (g & 1u);
+      const uint32_t f0 = f;
+      const int32_t u0 = u, v0 = v;
+      f = sw ? g : f;
+      g = sw ? 0u - f0 : g;
+      u = sw ? q : u;
+      v = sw ? r : v;
+      q = sw ? -u0 : q;
+      r = sw ? -v0 : r;
+      delta = sw ? -delta : delta;
+      // g odd: g += f, row g += row f  (then g is even)
+      const uint32_t odd = 0u - (g & 1u);
+      g += f & odd;
+      q += u & (int32_t)odd;
+      r += v & (int32_t)odd;
+      // g /= 2 (row f doubles in the 2^i scaling)
+      delta += 1;
+      g >>= 1;
+      u = (int32_t)((uint32_t)u << 1);  // (left shifts of negative ints are undefined in C++17)
+      v = (int32_t)((uint32_t)v << 1);
+    }
+    int32_t nF[BLS_NL], nD[BLS_NL];
+    by_lincomb(F, G, u, v, false, nF);
+    by_lincomb(F, G, q, r, false, G);
+    by_lincomb(D, E, u, v, true, nD);
+    by_lincomb(D, E, q, r, true, E);
+#pragma unroll
+    for (int j = 0; j < BLS_NL; j++) {
+      F[j] = nF[j];
+      D[j] = nD[j];
+    }
+  }
+  // f = +-1 (or p when x = 0, where d = 0): x^-1 = f d; |d| < 41 p, so f d + 42 p is a positive normalized value < 83 p
+  const bool neg = F[BLS_NL - 1] < 0;
+  fp y;
+  int64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < BLS_NL; j++) {
+    c += (int64_t)(neg ? -(int64_t)D[j] : (int64_t)D[j]) + 42 * (int64_t)FP_P.l[j];
+    if (j < BLS_NL - 1) {
+      y.l[j] = (uint32_t)c & BLS_MASK;
+      c >>= BLS_LB;
+    } else {
+      y.l[j] = (uint32_t)c;
+    }
+  }
+  // y = (aR)^-1 mod p in plain form; the Montgomery form of a^-1 is y R^2 = Mont(y, R^3) (output < 1.05 p)
+  return fp_mul(y, FP_R3);
+}
 BLS_HD fp fp_pow_p34(const fp& a) { return fp_pow_words(a, EXP_P_MINUS_3_DIV_4, 379); }
 
 // Big-endian 48-byte <-> canonical integer limbs (not Montgomery).  Returns false if value >= p.

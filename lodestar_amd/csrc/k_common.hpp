@@ -162,12 +162,17 @@ __device__ jac<F> jac_mul_u64_j(const jac<F>& P, uint64_t k) {
   return r;
 }
 
-// [r]P for the batch scalar encoded by the 64-bit word w (runtime.cpp `scalar words`): r = sum_i d_i 16^i with
-// the 16 odd digits d_i = 2 nibble_i(w) - 15 in {-15, ..., 15}, i.e. r = 2w + 1 - 2^64 -- a bijection between
-// the 2^64 words and 2^64 distinct odd scalars, so the random linear combination keeps blst's 2^-64
-// soundness.  Regular signed window: every lane runs the same 61 doublings and 22 additions (no
-// data-dependent branch, unlike double-and-add with a lane-varying scalar); the table of odd multiples
-// P, 3P, ..., 15P lives in HBM (SoA, tab[(e * 3 * WF + word) * n + i], WF = words of one coordinate).
+// [r]P for the batch scalar encoded by the 64-bit word w (runtime.cpp `scalar words`):
+//   r = a + b lambda (mod the group order),  lambda = -z^2 (curve.hpp endo_lambda: phi on G1, -psi^2 on G2),
+//   a = sum_k d_k 16^k over the 8 nibbles of w's low half, b the same over its high half, d = 2 nibble - 15 (odd,
+//   in [-15, 15]) -- so a = 2 lo + 1 - 2^32 and b = 2 hi + 1 - 2^32, odd 33-bit integers.
+// The 2^64 words give 2^64 distinct r mod the group order (a collision would be a lattice vector (a - a', b - b') of
+// x + y lambda = 0 with both coordinates below 2^33, but that lattice's shortest vectors, e.g. (z^2, 1), are ~2^127
+// long), so the random linear combination keeps blst's 2^-64 soundness, while [r]P costs 28 doublings (8 windows of
+// 4 bits, both halves sharing them: Straus) instead of the 60 of a 64-bit scalar.  Word 0 means r = 1 (CoreVerify),
+// which the callers take as P itself.  Regular signed windows: every lane runs the same doublings and additions (no
+// data-dependent branch); the table of odd multiples P, 3P, ..., 15P lives in HBM (SoA, tab[(e * 3 * WF + word) * n
+// + i], WF = words of one coordinate) and lambda is applied to the entry the high half picks.
 template <class F>
 __device__ __forceinline__ void tab_st(uint32_t* tab, uint32_t n, uint32_t i, int e, const jac<F>& v) {
   constexpr int WF = sizeof(F) / 4;
@@ -184,6 +189,12 @@ __device__ __forceinline__ jac<F> tab_ld(const uint32_t* tab, uint32_t n, uint32
   for (int w = 0; w < 3 * WF; w++) d[w] = tab[((size_t)e * 3 * WF + w) * n + i];
   return v;
 }
+// signed digit k (0..15) of word w: table entry (|d| - 1) / 2, sign
+BLS_HD int scalar_word_digit(uint64_t w, int k, bool& neg) {
+  const int d = 2 * (int)((w >> (4 * k)) & 15u) - 15;
+  neg = d < 0;
+  return (d < 0 ? -d : d) >> 1;
+}
 template <class F>
 __device__ jac<F> jac_mul_scalar_word(const jac<F>& P, uint64_t w, uint32_t* tab, uint32_t n, uint32_t i) {
   const jac<F> P2 = jac_dbl(P);
@@ -194,23 +205,20 @@ __device__ jac<F> jac_mul_scalar_word(const jac<F>& P, uint64_t w, uint32_t* tab
     t = jac_add(t, P2);
     tab_st(tab, n, i, e, t);
   }
-  auto digit = [&](int k, bool& neg) {
-    const int nib = (int)((w >> (4 * k)) & 15u);
-    const int d = 2 * nib - 15;
-    neg = d < 0;
-    return (d < 0 ? -d : d) >> 1;  // table entry of |d| = 2e + 1
+  const uint32_t ii = opaque_u32(i);  // table addresses recomputed per window, not hoisted and spilled
+  auto term = [&](int k, bool hi) {
+    bool neg;
+    const int e = scalar_word_digit(w, hi ? k + 8 : k, neg);
+    jac<F> q = tab_ld<F>(tab, n, ii, e);
+    if (hi) q = endo_lambda(q);
+    return neg ? jac_neg(q) : q;
   };
-  bool neg;
-  int e = digit(15, neg);
-  jac<F> r = tab_ld<F>(tab, n, i, e);
-  if (neg) r = jac_neg(r);
+  jac<F> r = jac_add(term(7, false), term(7, true));
 #pragma unroll 1
-  for (int k = 14; k >= 0; k--) {
+  for (int k = 6; k >= 0; k--) {
     r = jac_dbl(jac_dbl(jac_dbl(jac_dbl(r))));
-    e = digit(k, neg);
-    jac<F> q = tab_ld<F>(tab, n, i, e);
-    if (neg) q = jac_neg(q);
-    r = jac_add(r, q);
+    r = jac_add(r, term(k, false));
+    r = jac_add(r, term(k, true));
   }
   return r;
 }

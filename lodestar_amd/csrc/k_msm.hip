@@ -6,7 +6,8 @@
 //                  is deterministic); the lane then sums +-sig_i with mixed additions -> B[slice][t].  Lists keep
 //                  the wave's lanes busy on useful additions: ~len/8 per lane instead of len masked ones.
 //   k_msm_window   one lane per (range, window): W = sum_e (2e + 1) sum_{slices of the range} B_e
-//   k_msm_horner   one lane per range: S = sum_k 16^k W_k, written in the layout k_group_check reads
+//   k_msm_horner   two lanes per range: S_a and lambda S_b (8-window Horner passes, msm.hpp), then S = their sum,
+//                  written in the layout k_group_check reads
 // Sets outside the batch equation (include == 0) and infinity signatures contribute nothing, as in the
 // per-set scaling this replaces.
 #include "k_common.hpp"
@@ -72,11 +73,20 @@ STAGE_KERNEL void k_msm_window(const uint32_t* range_slices, uint32_t n_ranges, 
   st_g2j(W, n_ranges * MSM_WINDOWS, q, Wk);
 }
 
-STAGE_KERNEL void k_msm_horner(const uint32_t* W, uint32_t n_ranges, uint32_t* S) {
-  const uint32_t r = blockIdx.x * WAVE + threadIdx.x;
-  if (r >= n_ranges) return;
+// lane pair (r, part) of one wave: part 1 leaves lambda S_b in its range's (already consumed) window-8 slot of W,
+// part 0 adds it after the barrier.  W is written and read within the workgroup, so no lane returns early.
+STAGE_KERNEL void k_msm_horner(uint32_t* W, uint32_t n_ranges, uint32_t* S) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  const uint32_t r = q >> 1, part = q & 1;
+  const bool on = r < n_ranges;
   const uint32_t nw = n_ranges * MSM_WINDOWS;
-  st_g2j(S, n_ranges, r, msm_horner([&](int k) { return ld_g2j(W, nw, r * MSM_WINDOWS + k); }));
+  g2j H;
+  if (on) {
+    H = msm_horner_half([&](int k) { return ld_g2j(W, nw, r * MSM_WINDOWS + k); }, (int)part);
+    if (part) st_g2j(W, nw, r * MSM_WINDOWS + MSM_WINDOWS / 2, H);
+  }
+  __syncthreads();
+  if (on && !part) st_g2j(S, n_ranges, r, jac_add(H, ld_g2j(W, nw, r * MSM_WINDOWS + MSM_WINDOWS / 2)));
 }
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
@@ -87,5 +97,5 @@ void launch_sig_msm(const PipelineBuffers& b, const uint32_t* slices, uint32_t n
   if (n_slices) hipLaunchKernelGGL(k_msm_bucket, dim3(n_slices), dim3(MSM_LANES), 0, st, b, slices, n_slices, B);
   hipLaunchKernelGGL(k_msm_window, grid_for(n_ranges * MSM_WINDOWS), dim3(WAVE), 0, st, range_slices, n_ranges, B,
                      n_slices, W);
-  hipLaunchKernelGGL(k_msm_horner, grid_for(n_ranges), dim3(WAVE), 0, st, W, n_ranges, S);
+  hipLaunchKernelGGL(k_msm_horner, grid_for(2 * n_ranges), dim3(WAVE), 0, st, W, n_ranges, S);
 }

@@ -141,6 +141,10 @@ struct Task {
 // The device's pipeline streams, shared by its slots: one per branch of a run's DAG (run_shard).  Runs of different
 // slots queue behind each other per branch, so the chip always has the next run's work while one run's tail drains.
 enum { kSig = 0, kMsg = 1, kPk = 2, kTail = 3, kStreams = 4 };
+// streams created with the device's highest priority (bit k = stream k); see blsgpu_init
+#ifndef BLSGPU_STREAM_PRIO
+#define BLSGPU_STREAM_PRIO ((1 << kMsg) | (1 << kTail))
+#endif
 
 struct Device {
   int id = 0;
@@ -1512,7 +1516,18 @@ int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
       ctx->devs.push_back(d);
       HIPCHK(hipSetDevice(id));
       HIPCHK(hipStreamCreateWithFlags(&d->table_stream, hipStreamNonBlocking));
-      for (hipStream_t& st : d->st) HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      // The message branch (hash_to_G2 -> Miller lines -> Miller accumulation -> F reduction) is the serial chain that
+      // bounds a device's throughput (~70% of the work, one in-order stream shared by the runs in flight): its stream
+      // gets the device's highest priority, so its kernels take free SIMDs first and the signature / pubkey branches
+      // fill the gaps its tails leave, instead of stretching the chain; so does the short tail (final
+      // exponentiations -> results), which returns finished calls sooner.  (C2, interleaved A/B: 2.90M sets/s with no
+      // priorities, 2.94M message stream, 2.945M message + tail; profiles/r03_ab6_stream_priority.txt.)
+      int prio_lo = 0, prio_hi = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+      for (int k = 0; k < kStreams; k++) {
+        const bool high = (BLSGPU_STREAM_PRIO & (1 << k)) != 0;
+        HIPCHK(hipStreamCreateWithPriority(&d->st[k], hipStreamNonBlocking, high ? prio_hi : prio_lo));
+      }
     }
   } catch (HipError&) {
     blsgpu_destroy(ctx);

@@ -76,3 +76,21 @@ def b2f12(b):
     vals = [fromb(b[48 * i : 48 * i + 48]) for i in range(12)]
     c2 = [(vals[2 * i], vals[2 * i + 1]) for i in range(6)]
     return ((c2[0], c2[1], c2[2]), (c2[3], c2[4], c2[5]))
+
+
+LAMBDA = None
+
+
+def r_of_word(w, raw=False):
+    """Batch scalar of a 64-bit word (runtime.cpp / k_common.hpp jac_mul_scalar_word): r = a + b lambda mod the
+    group order, lambda = -z^2 (phi on G1, -psi^2 on G2), a = 2 lo + 1 - 2^32, b = 2 hi + 1 - 2^32 of the word's
+    32-bit halves; word 0 = r = 1 (CoreVerify) unless `raw` (the digits' value, as jac_mul_scalar_word computes)."""
+    from oracle import bls12_381 as bls
+
+    if w == 0 and not raw:
+        return 1
+    z = 0xD201000000010000
+    lam = (-z * z) % bls.R
+    a = 2 * (w & 0xFFFFFFFF) + 1 - 2**32
+    b = 2 * (w >> 32) + 1 - 2**32
+    return (a + b * lam) % bls.R

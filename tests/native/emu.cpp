@@ -57,20 +57,23 @@ static fp12 load12(const uint8_t* b) {
   return f;
 }
 
-// the device's regular signed-window scalar multiplication (k_common.hpp jac_mul_scalar_word), host table
+// the device's regular signed-window scalar multiplication (k_common.hpp jac_mul_scalar_word: r = a + b lambda,
+// Straus over the two 8-digit halves), host table
 template <class F>
 static jac<F> emu_mul_scalar_word(const jac<F>& P, uint64_t w) {
   jac<F> tab[8];
   const jac<F> P2 = jac_dbl(P);
   tab[0] = P;
   for (int e = 1; e < 8; e++) tab[e] = jac_add(tab[e - 1], P2);
-  auto pick = [&](int k) {
-    const int d = 2 * (int)((w >> (4 * k)) & 15u) - 15;
+  auto pick = [&](int k, bool hi) {
+    const int d = 2 * (int)((w >> (4 * (hi ? k + 8 : k))) & 15u) - 15;
     jac<F> q = tab[(d < 0 ? -d : d) >> 1];
+    if (hi) q = endo_lambda(q);
     return d < 0 ? jac_neg(q) : q;
   };
-  jac<F> r = pick(15);
-  for (int k = 14; k >= 0; k--) r = jac_add(jac_dbl(jac_dbl(jac_dbl(jac_dbl(r)))), pick(k));
+  jac<F> r = jac_add(pick(7, false), pick(7, true));
+  for (int k = 6; k >= 0; k--)
+    r = jac_add(jac_add(jac_dbl(jac_dbl(jac_dbl(jac_dbl(r)))), pick(k, false)), pick(k, true));
   return r;
 }
 // The bucket MSM of k_msm.hip (msm.hpp) over n affine points with scalar words w: buckets filled in set order
@@ -84,6 +87,7 @@ static g2j emu_msm_core(const g2a* P, const uint64_t* w, const uint8_t* active, 
     for (int k = 0; k < MSM_WINDOWS; k++) {
       bool neg;
       const uint32_t e = msm_bucket(w[i], k, neg);
+      if (e == MSM_NO_BUCKET) continue;
       g2a q = P[i];
       if (neg) q.y = fp2_neg(q.y);
       B[k][e] = jac_add_aff(B[k][e], q);
@@ -101,6 +105,19 @@ int emu_msm(const uint8_t* pts192, const uint64_t* w, const uint8_t* active, int
   for (int i = 0; i < n; i++) P[i] = load_g2(pts192 + 192 * (size_t)i);
   g2a a;
   if (!jac_to_aff(emu_msm_core(P, w, active, n), a)) return 0;
+  g2a_to_be192(a, out192);
+  return 1;
+}
+// the batch-scalar multiplications themselves (r = a + b lambda of word w; word 0 = the digits' value too)
+int emu_g1_mul_word(const uint8_t* pk96, uint64_t w, uint8_t* out96) {
+  g1a a;
+  if (!jac_to_aff(emu_mul_scalar_word(jac_from_aff(load_g1(pk96)), w), a)) return 0;
+  g1a_to_be96(a, out96);
+  return 1;
+}
+int emu_g2_mul_word(const uint8_t* sig192, uint64_t w, uint8_t* out192) {
+  g2a a;
+  if (!jac_to_aff(emu_mul_scalar_word(jac_from_aff(load_g2(sig192)), w), a)) return 0;
   g2a_to_be192(a, out192);
   return 1;
 }

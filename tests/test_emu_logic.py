@@ -42,6 +42,25 @@ def test_fp_ops():
         assert fromb(o.raw) == (pow(a, P - 2, P))
 
 
+def test_fp_inv_divsteps_edges_and_random():
+    """fp_inv (Bernstein-Yang divsteps, fp.hpp) against x^(p-2) at the edges of its 40-batch bound: 0, 1, 2, p - 1,
+    powers of two, values whose gcd chain is long (Fibonacci-like neighbours of p), all-ones limbs, and 1,500 random
+    elements."""
+    L = lib()
+    o = buf(48)
+    fib = [1, 1]
+    while fib[-1] < P:
+        fib.append(fib[-1] + fib[-2])
+    vals = [0, 1, 2, 3, P - 1, P - 2, (P - 1) // 2, (P + 1) // 2, 2**380 % P, 2**28, 2**364 % P, (2**381 - 1) % P,
+            int("0fffffff" * 12, 16) % P, fib[-2] % P, fib[-3] % P, (P * fib[-4]) // fib[-3]]
+    vals += [2**k % P for k in range(0, 381, 17)]
+    r2 = random.Random(2024)
+    vals += [r2.randrange(P) for _ in range(1500)]
+    for a in vals:
+        L.emu_fp_inv(fpb(a), o)
+        assert fromb(o.raw) == (pow(a, P - 2, P) if a % P else 0), a
+
+
 def test_fp2_ops_and_sqrt():
     L = lib()
     o = buf(96)
@@ -204,8 +223,27 @@ def test_key_validate_matches_c_oracle():
 
 
 def _r_of_word(w):
-    """Batch scalar of a 64-bit word (runtime.cpp / k_common.hpp): r = 2w + 1 - 2^64, word 0 = r = 1."""
-    return 1 if w == 0 else 2 * w + 1 - 2**64
+    from tests.emu_helpers import r_of_word
+
+    return r_of_word(w)
+
+
+def test_batch_scalar_word_multiplication():
+    """k_common.hpp jac_mul_scalar_word (host copy): [a]P + [b] lambda(P) with lambda = phi on G1 and -psi^2 on
+    G2 equals [r]P for r = a + b lambda mod the group order -- both groups use the same r."""
+    from tests.emu_helpers import b2g1, g1b, r_of_word
+
+    L = lib()
+    L.emu_g1_mul_word.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    L.emu_g2_mul_word.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    r2 = random.Random(91)
+    P = bls.g1_mul(bls.G1_GEN, r2.randrange(1, bls.R))
+    Q = bls.g2_mul(bls.G2_GEN, r2.randrange(1, bls.R))
+    o1, o2 = buf(96), buf(192)
+    for w in [0, 1, 2**32 - 1, 2**32, 2**64 - 1, 0x8000000080000000] + [r2.getrandbits(64) for _ in range(6)]:
+        r = r_of_word(w, raw=True)
+        assert L.emu_g1_mul_word(g1b(P), w, o1) == 1 and b2g1(o1.raw) == bls.g1_mul(P, r), hex(w)
+        assert L.emu_g2_mul_word(g2b(Q), w, o2) == 1 and b2g2(o2.raw) == bls.g2_mul(Q, r), hex(w)
 
 
 def test_bucket_msm_matches_sum_of_scalings():

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from oracle import bls12_381 as bls
-from tests.emu_helpers import b2f12, b2g1, b2g2, f12b, fpb, fromb, g1b, g2b
+from tests.emu_helpers import b2f12, b2g1, b2g2, f12b, fpb, fromb, g1b, g2b, r_of_word
 
 pytestmark = pytest.mark.gpu
 
@@ -229,8 +229,8 @@ def test_verify_table_mode_aggregate(ctx):
 
 
 def test_debug_scalar_word_mul():
-    """The batch scalar of word w is r = 2w + 1 - 2^64 (k_common.hpp jac_mul_scalar_word): G1 and G2 against
-    the oracle's plain scalar multiplication, including the extreme words."""
+    """The batch scalar of word w is r = a + b lambda (k_common.hpp jac_mul_scalar_word, tests/emu_helpers.py
+    r_of_word): G1 and G2 against the oracle's plain scalar multiplication, including the extreme words."""
     from lodestar_amd.native import Context
 
     ctx = Context([0])
@@ -245,7 +245,7 @@ def test_debug_scalar_word_mul():
         o2, s2 = ctx.debug_op(9, inp2, 200, 2880)
         assert (s1 == 0).all() and (s2 == 0).all()
         for k, w in enumerate(words):
-            r = (2 * w + 1 - 2**64) % bls.R
+            r = r_of_word(w, raw=True)  # the op scales by the digits of every word, 0 included
             assert o1[1440 * k: 1440 * k + 96] == bls.g1_serialize(bls.g1_mul(P, r))
             assert o2[2880 * k: 2880 * k + 192] == bls.g2_serialize(bls.g2_mul(Q, r))
     finally:
