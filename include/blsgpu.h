@@ -145,8 +145,9 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * accumulator sharing its Fp12 squarings, 1..64; default 0 = by run size: 1 below 131072 pairings, 2 below
  * 262144, else 4), "merge_sets" (a runtime slot merges calls
  * already queued on its device into one pipeline run of up to this many sets -- jobs and results stay per
- * call -- default 131072, 0 = never), "pipeline_depth" (runs a device keeps in flight, default 2: its slots share
- * the device's streams, so a further run would only queue behind them), "merge_wait_us" (while runs are in
+ * call -- default 131072, 0 = never), "pipeline_depth" (runs a device keeps in flight, default 3: consecutive runs
+ * alternate between the device's two stream pairs, so two runs' message chains overlap and a third run's decode /
+ * pubkey work fills the gaps; a deeper pipeline only queues), "merge_wait_us" (while runs are in
  * flight, a slot forming a run waits up to this long for more calls to merge, default 2000; an idle device starts
  * at once), "profile" (per-stage kernel times in
  * blsgpu_stats.stage_ms, 0/1), "group_policy" (0 = batch groups of >= group_sets sets, the default; 1 = the

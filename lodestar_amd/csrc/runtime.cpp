@@ -145,6 +145,13 @@ enum { kSig = 0, kMsg = 1, kPk = 2, kTail = 3, kStreams = 4 };
 #ifndef BLSGPU_STREAM_PRIO
 #define BLSGPU_STREAM_PRIO ((1 << kMsg) | (1 << kTail))
 #endif
+// Stream pairs (default): consecutive runs alternate between two (signature, message) stream pairs -- run parity p
+// uses st[2p] for its signature, pubkey and tail branches and st[2p + 1] (high priority) for its message branch --
+// so the message chains of the two runs in flight (pipeline_depth 2) overlap instead of queueing behind each other on
+// one message stream, the serial chain that bounded throughput.  0: one stream per branch, shared by all runs.
+#ifndef BLSGPU_STREAM_PAIRS
+#define BLSGPU_STREAM_PAIRS 1
+#endif
 
 struct Device {
   int id = 0;
@@ -165,6 +172,7 @@ struct Device {
   std::vector<Slot*> slots;
   std::vector<std::thread> workers;
   int runs_inflight = 0;  // under q_mu: runs taken by a slot whose batch pass has not completed
+  std::atomic<uint32_t> run_seq{0};  // run counter: the stream pair of a run (BLSGPU_STREAM_PAIRS)
 };
 
 inline uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
@@ -184,7 +192,7 @@ struct Options {  // snapshot taken at the start of each call
   int64_t miller_k = 0;  // pairings per Miller accumulator (shared squarings); 0 = by run size (miller_k_auto)
   int64_t merge_sets = 131072;  // queued calls a slot merges into one pipeline run (sets), 0 = never
   int64_t merge_wait_us = 2000;  // while runs are in flight, a slot waits this long for more calls to merge
-  int64_t pipeline_depth = 2;    // runs a device has in flight (taken by a slot, batch pass not yet complete)
+  int64_t pipeline_depth = 3;    // runs a device has in flight (taken by a slot, batch pass not yet complete)
   int64_t group_policy = 0;    // 0 = groups of >= group_sets sets; 1 = the reference pool's jobs / requests / chunks
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
@@ -528,7 +536,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   else
     in_bytes = o_pk + (size_t)n * 96;
   const size_t o_pk2 = al256(o_pk + (size_t)(n + 1) * 4);
-  sl.set_stream(d.st[kSig]);  // buffer growth of the batch pass, ordered before the input copy on the same stream
+  const int par = BLSGPU_STREAM_PAIRS ? (int)(d.run_seq.fetch_add(1) & 1u) : 0;
+  hipStream_t s = BLSGPU_STREAM_PAIRS ? d.st[2 * par] : d.st[kSig];
+  sl.set_stream(s);  // buffer growth of the batch pass, ordered before the input copy on the same stream
   sl.h_in.ensure(in_bytes);
   sl.d_in.ensure(in_bytes);
   uint8_t* const hin = sl.h_in.p;
@@ -593,7 +603,6 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   const size_t per_set = W_G2A + W_G1J + W_G1A + W_FP12 + 8 * W_G1J + 2 * W_FP + (merged ? W_G1A : 0);
   sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * (W_G2A + W_G2J + W_FP + 14 * W_FP + 2 * W_G2J));
   sl.d_lines.ensure((size_t)nm * kMillerLineWords);
-  hipStream_t s = d.st[kSig];
   uint8_t* const din = sl.d_in.p;
   uint8_t* const d_ok0 = sl.d_res.p + o_ok;
 
@@ -652,15 +661,17 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.job_err = reinterpret_cast<int8_t*>(sl.d_res.p);
 
   // ---- kernel pipeline ------------------------------------------------------------------------------------
-  // DAG of one run on the device's four streams (shared by its slots: the next run of another slot queues behind
-  // this one per branch, so the chip has its work while this run's tail drains):
-  //   signatures (kSig): input copy -> decode -> [pubkeys done] job mask -> MSM -> MillerLoop(-g1, S_g)
-  //   messages (kMsg):   hash_to_G2 -> affine -> Miller lines -> [job mask done] Miller accumulation -> F reduction
-  //   pubkeys (kPk):     aggregate -> r_i pk_i -> affine
-  //   tail (kTail):      [S_g Miller + F done] final exponentiation per group -> results copy
-  // An isolated call's critical path is the longer of the branches plus the final exponentiation.
+  // DAG of one run on the device's streams (shared by its slots):
+  //   signatures (s):    input copy -> decode -> [pubkeys done] job mask -> MSM -> MillerLoop(-g1, S_g)
+  //   messages (sm):     hash_to_G2 -> affine -> Miller lines -> [job mask done] Miller accumulation -> F reduction
+  //   pubkeys (sp):      aggregate -> r_i pk_i -> affine
+  //   tail (stl):        [S_g Miller + F done] final exponentiation per group -> results copy
+  // With stream pairs (BLSGPU_STREAM_PAIRS) the pubkey and tail branches run on the run's signature stream (they are
+  // short next to the message branch) and consecutive runs use the other pair; without, each branch has its own
+  // stream shared by every run.  An isolated call's critical path is the message branch plus the final exponentiation.
   const bool prof = opt.profile;
-  hipStream_t sm = d.st[kMsg], sp = d.st[kPk], stl = d.st[kTail];
+  hipStream_t sm = BLSGPU_STREAM_PAIRS ? d.st[2 * par + 1] : d.st[kMsg], sp = BLSGPU_STREAM_PAIRS ? s : d.st[kPk],
+              stl = BLSGPU_STREAM_PAIRS ? s : d.st[kTail];
   auto beg = [&](int k, hipStream_t st) {
     if (prof) HIPCHK(hipEventRecord(sl.ev[2 * k], st));
   };
