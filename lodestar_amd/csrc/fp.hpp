@@ -234,6 +234,33 @@ BLS_HD fp fp_add_nr(const fp& a, const fp& b) {
   return s;
 }
 
+// a + b with the carries propagated but no reduction: normalized limbs, value <= a + b (an operand-side sum)
+BLS_HD fp fp_add_norm(const fp& a, const fp& b) {
+  fp s;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL - 1; i++) {
+    uint32_t v = a.l[i] + b.l[i] + c;
+    s.l[i] = v & BLS_MASK;
+    c = v >> BLS_LB;
+  }
+  s.l[BLS_NL - 1] = a.l[BLS_NL - 1] + b.l[BLS_NL - 1] + c;
+  return s;
+}
+
+// 8p with every limb but the top borrowed up into [2^28 - 1, 2^29): a + FP_8P_K - b has no negative limb for any
+// normalized b of value <= 4p (its top limb stays below FP_8P_K's) -- the lazy subtraction below
+BLS_CONST fp FP_8P_K = {{0x1ffd5558, 0x1f7ffffe, 0x1ffffdce, 0x1fff58a8, 0x1120f55e, 0x107b587a, 0x1b398694, 0x19c2895e, 0x13ba5c26, 0x15d66bb1, 0x1d3db219, 0x134d258c, 0x1f51cbfe, 0x000d0087}};
+// a - b (mod p) as a lazy fp_mul operand: a + 8p - b limb by limb, no carries, no reduction.  a: limbs < 2^29;
+// b: normalized, value <= 4p.  Result: limbs < 2^30, value < a + 8p (only as an operand of fp_mul, whose column sums
+// and output bound allow limbs < 2^30 and values < 16p -- never stored).
+BLS_HD fp fp_sub_k8(const fp& a, const fp& b) {
+  fp s;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) s.l[i] = a.l[i] + FP_8P_K.l[i] - b.l[i];
+  return s;
+}
+
 BLS_HD fp fp_sub(const fp& a, const fp& b) {
   // a + 2p - b  in [0, 4p]  -> conditional subtract 2p
   fp s;

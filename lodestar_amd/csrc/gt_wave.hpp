@@ -16,68 +16,10 @@
 // oracle pins; tests/test_gpu_pipeline.py compares both against oracle/bls12_381.py.
 #pragma once
 #include "pairing.hpp"
+#include "lacc.hpp"
 
 #define GTW_LANES 128
 #define GTW_FP12 (12 * BLS_NL)
-
-// ---------------------------------------------------------------------------------------------------
-// Lazily reduced signed sums of Fp values (each <= 2p, normalized limbs): limb sums without carries,
-// one carry pass and one quotient-estimate reduction at the end.  At most 15 terms per side.
-// ---------------------------------------------------------------------------------------------------
-struct lacc {
-  uint32_t pos[BLS_NL], neg[BLS_NL];
-};
-BLS_INL void lacc_init(lacc& a) {
-#pragma unroll
-  for (int i = 0; i < BLS_NL; i++) a.pos[i] = a.neg[i] = 0;
-}
-BLS_INL void lacc_add(lacc& a, const fp& x) {
-#pragma unroll
-  for (int i = 0; i < BLS_NL; i++) a.pos[i] += x.l[i];
-}
-BLS_INL void lacc_sub(lacc& a, const fp& x) {
-#pragma unroll
-  for (int i = 0; i < BLS_NL; i++) a.neg[i] += x.l[i];
-}
-// 32 p in 28-bit limbs
-BLS_INL uint32_t fp_p32_limb(int i) {
-  uint32_t lo = (FP_P.l[i] << 5) & BLS_MASK;
-  if (i == BLS_NL - 1) lo = FP_P.l[i] << 5;
-  return lo | (i ? (FP_P.l[i - 1] >> (BLS_LB - 5)) : 0u);
-}
-// pos - neg (mod p), result <= 2p normalized
-BLS_INL fp lacc_fin(const lacc& a) {
-  uint32_t v[BLS_NL];
-  int64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < BLS_NL; i++) {
-    int64_t d = (int64_t)a.pos[i] + (int64_t)fp_p32_limb(i) - (int64_t)a.neg[i] + c;
-    if (i < BLS_NL - 1) {
-      v[i] = (uint32_t)d & BLS_MASK;
-      c = d >> BLS_LB;
-    } else {
-      v[i] = (uint32_t)d;  // value < 48 p < 2^387: top limb < 2^23
-    }
-  }
-  // q ~ floor(v / p), never above it and at most one below (p / 2^336 ~ 2^44.7: the 51-bit estimate's
-  // error is far below 1), so v - q p is in [0, 2p)
-  const double vhi = (double)v[BLS_NL - 1] * 268435456.0 + (double)v[BLS_NL - 2];
-  const double phi = (double)FP_P.l[BLS_NL - 1] * 268435456.0 + (double)FP_P.l[BLS_NL - 2] + 1.0;
-  const uint32_t q = (uint32_t)(vhi / phi);
-  fp r;
-  c = 0;
-#pragma unroll
-  for (int i = 0; i < BLS_NL; i++) {
-    int64_t d = (int64_t)v[i] - (int64_t)((uint64_t)q * FP_P.l[i]) + c;
-    if (i < BLS_NL - 1) {
-      r.l[i] = (uint32_t)d & BLS_MASK;
-      c = d >> BLS_LB;
-    } else {
-      r.l[i] = (uint32_t)d;
-    }
-  }
-  return r;
-}
 
 // ---------------------------------------------------------------------------------------------------
 // LDS access (Fp index q of a buffer: words q*14 .. q*14+13)
@@ -94,10 +36,11 @@ BLS_INL void lds_st(uint32_t* b, int q, const fp& v) {
 }
 BLS_INL void gtw_sync() { __syncthreads(); }
 
-// (x0 + x1 u)^2 = (x0 + x1)(x0 - x1) + (2 x0) x1 u : operands of component `comp`'s single product
+// (x0 + x1 u)^2 = (x0 + x1)(x0 - x1) + (2 x0) x1 u : operands of component `comp`'s single product.  x0, x1:
+// normalized limbs, values <= 4p; the operands are lazy (limbs < 2^30, values < 12p: fp_mul's contract)
 BLS_INL void sqr_operands(const fp& x0, const fp& x1, int comp, fp& X, fp& Y) {
   X = comp ? fp_add_nr(x0, x0) : fp_add_nr(x0, x1);
-  Y = comp ? x1 : fp_sub(x0, x1);
+  Y = comp ? x1 : fp_sub_k8(x0, x1);
 }
 // Karatsuba component c of (a0 + a1 u)(b0 + b1 u): c0 = a0 b0, c1 = a1 b1, c2 = (a0 + a1)(b0 + b1)
 BLS_INL void kara_operands(const fp& a0, const fp& a1, const fp& b0, const fp& b1, int c, fp& X, fp& Y) {
@@ -170,8 +113,10 @@ __device__ void gtw_mul(uint32_t* C, const uint32_t* A, const uint32_t* B, uint3
 // D = A^2 in the cyclotomic subgroup (Granger-Scott, as fp12_cyclotomic_sqr in tower.hpp): the w-pairs
 // (k, k+3) are Fp4 elements; 9 Fp2 squarings = 18 Fp products, then 12 recombination lanes.
 // ---------------------------------------------------------------------------------------------------
+// PH: bit 0 = the product phase, bit 1 = the recombination phase (the latency probe times them apart)
+template <int PH = 3>
 __device__ void gtw_cyc_sqr(uint32_t* D, const uint32_t* A, uint32_t* S, uint32_t t) {
-  if (t < 18) {
+  if ((PH & 1) && t < 18) {
     const int p = t / 6, sq = (t % 6) >> 1, comp = t & 1;
     fp x0, x1;
     if (sq == 0) {
@@ -181,65 +126,48 @@ __device__ void gtw_cyc_sqr(uint32_t* D, const uint32_t* A, uint32_t* S, uint32_
       x0 = lds_ld(A, 2 * p + 6);
       x1 = lds_ld(A, 2 * p + 7);
     } else {
-      x0 = fp_add(lds_ld(A, 2 * p), lds_ld(A, 2 * p + 6));
-      x1 = fp_add(lds_ld(A, 2 * p + 1), lds_ld(A, 2 * p + 7));
+      x0 = fp_add_norm(lds_ld(A, 2 * p), lds_ld(A, 2 * p + 6));  // <= 4p, normalized: sqr_operands' contract
+      x1 = fp_add_norm(lds_ld(A, 2 * p + 1), lds_ld(A, 2 * p + 7));
     }
     fp X, Y;
     sqr_operands(x0, x1, comp, X, Y);
     lds_st(S, t, fp_mul(X, Y));
   }
   gtw_sync();
-  if (t < 12) {
+  if ((PH & 2) && t < 12) {
+    // Output k, component comp: 3 X -+ 2 z with X a signed sum of the pair's six products (t0r, t0i, t1r, t1i, sr, si)
+    // = S[6p .. 6p + 5].  kind 0: c0 = xi t1 + t0 = (t1r - t1i + t0r) + (t1r + t1i + t0i) u; kind 1: c1 = s - t0 - t1;
+    // kind 2: xi c1 = (c1r - c1i) + (c1r + c1i) u.  The signs come from a table (bit j of POS / NEG: product j enters
+    // with + / -), so the twelve lanes run ONE instruction stream: no divergent paths per kind and component.
     const int k = t >> 1, comp = t & 1;
-    // output k: pair, kind (0: c0 = xi t1 + t0, 1: c1 = s^2 - t0 - t1, 2: xi c1), sign of the 2 f_k term
     const int p = (k == 0 || k == 3) ? 0 : ((k == 2 || k == 5) ? 1 : 2);
     const int kind = (k == 0 || k == 2 || k == 4) ? 0 : (k == 1 ? 2 : 1);
-    const fp t0r = lds_ld(S, 6 * p), t0i = lds_ld(S, 6 * p + 1);
-    const fp t1r = lds_ld(S, 6 * p + 2), t1i = lds_ld(S, 6 * p + 3);
-    const fp sr = lds_ld(S, 6 * p + 4), si = lds_ld(S, 6 * p + 5);
-    lacc acc;
-    lacc_init(acc);
+    // sign masks over j = t0r, t0i, t1r, t1i, sr, si: 6 bits per entry e = 2 kind + comp
+    const int e = 2 * kind + comp;
+    const uint32_t pos = (uint32_t)(0xc1a810385ull >> (6 * e)) & 63u, neg = (uint32_t)(0x3e5285008ull >> (6 * e)) & 63u;
+    uint32_t ps[BLS_NL], ng[BLS_NL];
 #pragma unroll
-    for (int rep = 0; rep < 3; rep++) {
-      if (kind == 0) {
-        // c0 = (t1r - t1i + t0r) + (t1r + t1i + t0i) u
-        lacc_add(acc, t1r);
-        if (comp == 0) {
-          lacc_sub(acc, t1i);
-          lacc_add(acc, t0r);
-        } else {
-          lacc_add(acc, t1i);
-          lacc_add(acc, t0i);
-        }
-      } else if (kind == 1) {
-        // c1 = (sr - t0r - t1r) + (si - t0i - t1i) u
-        lacc_add(acc, comp ? si : sr);
-        lacc_sub(acc, comp ? t0i : t0r);
-        lacc_sub(acc, comp ? t1i : t1r);
-      } else {
-        // xi c1 = (c1r - c1i) + (c1r + c1i) u
-        lacc_add(acc, sr);
-        lacc_sub(acc, t0r);
-        lacc_sub(acc, t1r);
-        if (comp == 0) {
-          lacc_sub(acc, si);
-          lacc_add(acc, t0i);
-          lacc_add(acc, t1i);
-        } else {
-          lacc_add(acc, si);
-          lacc_sub(acc, t0i);
-          lacc_sub(acc, t1i);
-        }
+    for (int i = 0; i < BLS_NL; i++) ps[i] = ng[i] = 0;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      const uint32_t mp = 0u - ((pos >> j) & 1u), mn = 0u - ((neg >> j) & 1u);
+      const uint32_t* src = S + (6 * p + j) * BLS_NL;
+#pragma unroll
+      for (int i = 0; i < BLS_NL; i++) {
+        const uint32_t v = src[i];
+        ps[i] += v & mp;
+        ng[i] += v & mn;
       }
     }
-    // cyc_fix_sub: 3 t - 2 z (outputs 0, 2, 4), cyc_fix_add: 3 t + 2 z (outputs 1, 3, 5)
-    const fp z = lds_ld(A, t);
-    if (k & 1) {
-      lacc_add(acc, z);
-      lacc_add(acc, z);
-    } else {
-      lacc_sub(acc, z);
-      lacc_sub(acc, z);
+    // 3 X -+ 2 z: at most 3 products per side times 3, plus 2 z: <= 11 terms of < 2^28 per limb
+    const uint32_t* zs = A + t * BLS_NL;
+    const uint32_t mz = (k & 1) ? ~0u : 0u;
+    lacc acc;
+#pragma unroll
+    for (int i = 0; i < BLS_NL; i++) {
+      const uint32_t z2 = zs[i] << 1;
+      acc.pos[i] = 3 * ps[i] + (z2 & mz);
+      acc.neg[i] = 3 * ng[i] + (z2 & ~mz);
     }
     lds_st(D, t, lacc_fin(acc));
   }

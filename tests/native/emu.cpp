@@ -4,6 +4,7 @@
 #include <string.h>
 #include "../../lodestar_amd/csrc/ops.hpp"
 #include "../../lodestar_amd/csrc/msm.hpp"
+#include "../../lodestar_amd/csrc/lacc.hpp"
 
 #if defined(BLS_COUNT_OPS)
 unsigned long long bls_count_mul = 0, bls_count_sqr = 0, bls_count_half = 0;
@@ -120,6 +121,26 @@ int emu_g2_mul_word(const uint8_t* sig192, uint64_t w, uint8_t* out192) {
   if (!jac_to_aff(emu_mul_scalar_word(jac_from_aff(load_g2(sig192)), w), a)) return 0;
   g2a_to_be192(a, out192);
   return 1;
+}
+// lacc_fin on raw limb sums (14 + 14 words), raw limbs out
+void emu_lacc_fin(const uint32_t* pos, const uint32_t* neg, uint32_t* out14) {
+  lacc a;
+  for (int i = 0; i < BLS_NL; i++) {
+    a.pos[i] = pos[i];
+    a.neg[i] = neg[i];
+  }
+  const fp r = lacc_fin(a);
+  for (int i = 0; i < BLS_NL; i++) out14[i] = r.l[i];
+}
+// the cooperative squaring's lazy operands: Mont((x0 + x1) (x0 - x1)) with x0 - x1 as fp_sub_k8, raw limbs in / out
+void emu_sqr_operands_mul(const uint32_t* x0, const uint32_t* x1, uint32_t* out14) {
+  fp a, b;
+  for (int i = 0; i < BLS_NL; i++) {
+    a.l[i] = x0[i];
+    b.l[i] = x1[i];
+  }
+  const fp r = fp_mul(fp_add_nr(a, b), fp_sub_k8(a, b));
+  for (int i = 0; i < BLS_NL; i++) out14[i] = r.l[i];
 }
 #if defined(BLS_COUNT_OPS)
 // bucket MSM over n distinct points (the count covers the MSM only, not the point loads)

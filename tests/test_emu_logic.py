@@ -326,3 +326,41 @@ def test_hash_to_g2_two_lane_split_matches_oracle():
         m = bytes([j * 37 % 256]) * 32 if j < 3 else random.Random(j).randbytes(32)
         assert L.emu_hash_to_g2_split(m, out) == 1
         assert b2g2(out.raw) == bls.hash_to_g2(m)
+
+
+def _raw(v):
+    return [(v >> (28 * i)) & 0xFFFFFFF if i < 13 else v >> (28 * 13) for i in range(14)]
+
+
+def _val(l):
+    return sum(int(x) << (28 * i) for i, x in enumerate(l))
+
+
+def test_lacc_fin_and_lazy_operands():
+    """gt_wave.hpp's recombination (lacc.hpp lacc_fin: carry pass, integer quotient estimate, one conditional
+    subtraction) at the edges of its contract -- up to 15 terms of 2p per side, limb sums at their maxima -- and the
+    cooperative squaring's lazy operands (fp_sub_k8: x0 + 8p - x1 unreduced) for values up to 4p, against Python."""
+    L = lib()
+    r2 = random.Random(515)
+    A32 = ctypes.c_uint32 * 14
+    out = A32()
+    R_INV = pow(2**392, -1, P)
+    for trial in range(3000):
+        npos, nneg = r2.randint(0, 15), r2.randint(0, 15)
+        terms_p = [r2.choice([0, 2 * P, P, r2.randrange(2 * P + 1)]) for _ in range(npos)]
+        terms_n = [r2.choice([0, 2 * P, P - 1, r2.randrange(2 * P + 1)]) for _ in range(nneg)]
+        pos = [sum(_raw(t)[i] for t in terms_p) for i in range(14)]
+        neg = [sum(_raw(t)[i] for t in terms_n) for i in range(14)]
+        if trial % 7 == 0:  # limb sums at their maxima: 15 normalized limbs of 2^28 - 1
+            pos = [15 * 0xFFFFFFF if i < 13 else 15 * _raw(2 * P)[13] for i in range(14)]
+        L.emu_lacc_fin(A32(*pos), A32(*neg), out)
+        v = _val(out)
+        assert all(x < 2**28 for x in out[:13]) and v <= 2 * P, trial
+        assert (v - (_val(pos) - _val(neg))) % P == 0, trial
+    for trial in range(2000):
+        x0 = r2.choice([0, 4 * P, 2 * P, r2.randrange(4 * P + 1)])
+        x1 = r2.choice([0, 4 * P, 2 * P, r2.randrange(4 * P + 1)])
+        L.emu_sqr_operands_mul(A32(*_raw(x0)), A32(*_raw(x1)), out)
+        v = _val(out)
+        assert all(x < 2**28 for x in out[:13]) and v < 2 * P, trial
+        assert v % P == (x0 + x1) * (x0 - x1) * R_INV % P, trial

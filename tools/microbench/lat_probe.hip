@@ -16,11 +16,13 @@
     }                                                                              \
   } while (0)
 
-enum { P_MUL, P_SQR, P_FP2MUL, P_INV, P_INVPOW, P_POW34, P_G2DBL, P_CYC, P_GMUL, P_GSPARSE, P_FINEXP, P_FP12INV, NP };
+enum { P_MUL, P_SQR, P_FP2MUL, P_INV, P_INVPOW, P_POW34, P_G2DBL, P_CYC, P_GMUL, P_GSPARSE, P_FINEXP, P_FP12INV, P_CYC1,
+       P_CYC2, P_SYNC, P_LACC, NP };
 static const char* NAMES[NP] = {"fp_mul", "fp_sqr", "fp2_mul", "fp_inv_divsteps", "fp_inv_pow", "fp_pow_p34",
                                 "g2_jac_dbl", "gtw_cyc_sqr", "gtw_mul", "gtw_mul_sparse", "gtw_final_exp",
-                                "fp12_inv_lane0"};
-static const int REPS[NP] = {256, 256, 128, 8, 4, 4, 32, 64, 32, 32, 1, 2};
+                                "fp12_inv_lane0", "gtw_cyc_sqr_products", "gtw_cyc_sqr_recombine", "gtw_sync",
+                                "lacc_fin_lane"};
+static const int REPS[NP] = {256, 256, 128, 8, 4, 4, 32, 64, 32, 32, 1, 2, 64, 64, 256, 256};
 
 __device__ __forceinline__ uint64_t now() { return wall_clock64(); }
 
@@ -59,6 +61,10 @@ __global__ __launch_bounds__(GTW_LANES) void k_probe(uint64_t* ticks, uint32_t s
         case P_GSPARSE: gtw_mul<true>(sh.F, sh.F, sh.L, sh.S, t); break;
         case P_FINEXP: gtw_final_exp(sh.F, sh.W, sh.S, t); break;
         case P_FP12INV: if (t == 0) gtw_from_reg(sh.G, fp12_inv(gtw_to_reg(sh.F))); break;
+        case P_CYC1: gtw_cyc_sqr<1>(sh.F, sh.F, sh.S, t); break;
+        case P_CYC2: gtw_cyc_sqr<2>(sh.F, sh.F, sh.S, t); break;
+        case P_SYNC: gtw_sync(); break;
+        case P_LACC: if (t == 0) { lacc q; for (int i = 0; i < BLS_NL; i++) { q.pos[i] = a.l[i]; q.neg[i] = b.l[i]; } a = lacc_fin(q); } break;
       }
     }
     gtw_sync();
