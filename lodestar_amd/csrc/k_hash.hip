@@ -5,6 +5,7 @@
 // N(d)) -> k_batch_inv(N(d)) -> k_hash_map (one SSWU map + isogeny per lane, two lanes per message) ->
 // k_hash_clear (sum, cofactor clearing; Jacobian H(m) + N(z)) -> k_batch_inv(N(z)) -> k_h_affine.
 #include "k_common.hpp"
+#include "g2_coop.hpp"
 
 #define W_HPREP (7 * 2 * W_FP)
 
@@ -80,12 +81,52 @@ STAGE_KERNEL_W(BLSGPU_WPE_HASH) void k_hash_clear(PipelineBuffers b) {
   st_fp(b.h_norm, b.nm, u, 0, fp2_norm(H.z));
 }
 
+// The same clearing for small runs, latency first: one 16-lane group per message (g2_coop.hpp), four per workgroup;
+// the two [|z|] chains run as cooperative doublings, the additions and psi maps on the group's lane 0, the slots as
+// in k_hash_clear (the order of clear_cofactor_g2_slots).
+#define HC_GROUPS (WAVE / G2C_LANES)
+__global__ __launch_bounds__(WAVE) void k_hash_clear_coop(PipelineBuffers b) {
+  __shared__ uint32_t lds[HC_GROUPS * G2C_WORDS];
+  const uint32_t tg = threadIdx.x % G2C_LANES, grp = threadIdx.x / G2C_LANES;
+  const uint32_t u = blockIdx.x * HC_GROUPS + grp;
+  const bool on = u < b.n_umsg;
+  uint32_t* g = lds + grp * G2C_WORDS;
+  const uint32_t qs = 2 * b.nm;
+  if (tg == 0 && on) {
+    const g2j Q = jac_add(ld_g2j(b.h_q, qs, 2 * u), ld_g2j(b.h_q, qs, 2 * u + 1));
+    st_g2j(b.h_q, qs, 2 * u, Q);
+    g2c_st_point(g, Q);
+  }
+  g2c_sync();
+  // A = [|z|] Q
+  g2c_mul_zabs(g, tg, on, [&] { return ld_g2j(b.h_q, qs, 2 * opaque_u32(u)); });
+  if (tg == 0 && on) {
+    const g2j A = g2c_ld_point(g), P = ld_g2j(b.h_q, qs, 2 * u);
+    const g2j psiP = g2_psi(P);
+    const g2j B = jac_add(A, jac_neg(psiP));
+    st_g2j(b.h_q, qs, 2 * u + 1, B);
+    st_g2j(b.h_jac, b.nm, u, jac_add(jac_add(g2_psi2(jac_dbl(P)), jac_neg(psiP)), jac_add(A, jac_neg(P))));  // C
+    g2c_st_point(g, B);
+  }
+  g2c_sync();
+  // D = [|z|] (A - psi(Q)); H = C + D
+  g2c_mul_zabs(g, tg, on, [&] { return ld_g2j(b.h_q, qs, 2 * opaque_u32(u) + 1); });
+  if (tg == 0 && on) {
+    const g2j H = jac_add(g2c_ld_point(g), ld_g2j(b.h_jac, b.nm, u));
+    st_g2j(b.h_jac, b.nm, u, H);
+    st_fp(b.h_norm, b.nm, u, 0, fp2_norm(H.z));
+  }
+}
+
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
-void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s) {
+void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s, bool coop) {
   if (!b.n_umsg) return;
   hipLaunchKernelGGL(k_hash_prep, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
   launch_batch_inv(b.h_norm, b.nm, 0, b.inv_buf, b.n_umsg, s);
   hipLaunchKernelGGL(k_hash_map, grid_for(2 * b.n_umsg), dim3(WAVE), 0, s, b, b.inv_buf);
-  hipLaunchKernelGGL(k_hash_clear, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
+  if (coop)
+    hipLaunchKernelGGL(k_hash_clear_coop, dim3((b.n_umsg + HC_GROUPS - 1) / HC_GROUPS), dim3(WAVE), 0, s, b);
+  else
+    hipLaunchKernelGGL(k_hash_clear, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
 }

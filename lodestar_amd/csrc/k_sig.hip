@@ -1,8 +1,10 @@
 // A8 Signature.fromBytes(.., validate=true) (decompress + psi subgroup check) and the r_i * sig_i scaling
 // of the random linear combination (A9), one lane per signature set.
 #include "k_common.hpp"
+#include "g2_coop.hpp"
 
-STAGE_KERNEL_W(BLSGPU_WPE_DEC) void k_sig_decode(PipelineBuffers b, uint32_t n_sets) {
+// check_group == false: the subgroup check is left to k_sig_subgroup_coop (small runs)
+STAGE_KERNEL_W(BLSGPU_WPE_DEC) void k_sig_decode(PipelineBuffers b, uint32_t n_sets, bool check_group) {
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets) return;
   uint8_t raw[192];
@@ -19,7 +21,8 @@ STAGE_KERNEL_W(BLSGPU_WPE_DEC) void k_sig_decode(PipelineBuffers b, uint32_t n_s
   }
   st_g2a(b.sig_aff, b.n, i, p);
   // subgroup check with P re-read from the output buffer (curve.hpp jac_mul_zabs_ld: no P across the chain)
-  if (st == BLS_OK && !inf && !g2_in_subgroup_ld([&] { return ld_g2a(b.sig_aff, b.n, opaque_u32(i)); })) {
+  if (check_group && st == BLS_OK && !inf &&
+      !g2_in_subgroup_ld([&] { return ld_g2a(b.sig_aff, b.n, opaque_u32(i)); })) {
     st = BLS_POINT_NOT_IN_GROUP;
     p.x = fp2_zero();
     p.y = fp2_zero();
@@ -44,10 +47,37 @@ STAGE_KERNEL void k_sig_scale(PipelineBuffers b, uint32_t n_sets, const uint32_t
   st_g2j(b.rsig, b.n, i, R);
 }
 
+// The subgroup check psi(P) == [z]P of the decoded signatures for small runs, latency first: one 16-lane group per
+// signature (g2_coop.hpp), the [|z|] chain as cooperative doublings, the additions and the comparison on the group's
+// lane 0.  A failing signature becomes POINT_NOT_IN_GROUP with a zero point, as in k_sig_decode.
+#define SG_GROUPS (WAVE / G2C_LANES)
+__global__ __launch_bounds__(WAVE) void k_sig_subgroup_coop(PipelineBuffers b, uint32_t n_sets) {
+  __shared__ uint32_t lds[SG_GROUPS * G2C_WORDS];
+  const uint32_t tg = threadIdx.x % G2C_LANES, grp = threadIdx.x / G2C_LANES;
+  const uint32_t i = blockIdx.x * SG_GROUPS + grp;
+  uint32_t* g = lds + grp * G2C_WORDS;
+  const bool on = i < n_sets && b.status[i] == BLS_OK && !(b.flags[i] & SF_SIG_INF);
+  if (tg == 0 && on) g2c_st_point(g, jac_from_aff(ld_g2a(b.sig_aff, b.n, i)));
+  g2c_sync();
+  g2c_mul_zabs(g, tg, on, [&] { return jac_from_aff(ld_g2a(b.sig_aff, b.n, opaque_u32(i))); });
+  if (tg == 0 && on) {
+    const g2j zP = jac_neg(g2c_ld_point(g));
+    if (!jac_eq(g2_psi(jac_from_aff(ld_g2a(b.sig_aff, b.n, i))), zP)) {
+      g2a z;
+      z.x = fp2_zero();
+      z.y = fp2_zero();
+      st_g2a(b.sig_aff, b.n, i, z);
+      b.status[i] = (int8_t)BLS_POINT_NOT_IN_GROUP;
+    }
+  }
+}
+
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
-void launch_sig_decode(const PipelineBuffers& b, uint32_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_sig_decode, grid_for(n), dim3(WAVE), 0, s, b, n);
+void launch_sig_decode(const PipelineBuffers& b, uint32_t n, hipStream_t s, bool coop) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_sig_decode, grid_for(n), dim3(WAVE), 0, s, b, n, !coop);
+  if (coop) hipLaunchKernelGGL(k_sig_subgroup_coop, dim3((n + SG_GROUPS - 1) / SG_GROUPS), dim3(WAVE), 0, s, b, n);
 }
 void launch_sig_scale(const PipelineBuffers& b, uint32_t n, hipStream_t s, const uint32_t* list) {
   if (n) hipLaunchKernelGGL(k_sig_scale, grid_for(n), dim3(WAVE), 0, s, b, n, list);

@@ -82,8 +82,10 @@ struct PipelineBuffers {
   uint8_t* include;   // [n]: set belongs to a clean job (enters the batch equation)
 };
 
-void launch_sig_decode(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
-void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s);  // over the unique messages
+// coop: small runs -- the [|z|] chains (subgroup check, cofactor clearing) as cooperative 16-lane doublings
+// (g2_coop.hpp), for latency
+void launch_sig_decode(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s, bool coop = false);
+void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s, bool coop = false);  // over the unique messages
 void launch_pk_aggregate(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 void launch_pk_finish(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 // batched affine conversions (Montgomery's simultaneous inversion, k_inv.hip): r_i pk_i -> pk_aff, H(m) -> h_aff

@@ -64,3 +64,30 @@ BLS_INL fp lacc_fin(const lacc& a) {
   return fp_csub_p(r);
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// LDS access (Fp index q of a buffer: words q*14 .. q*14+13)
+// ---------------------------------------------------------------------------------------------------
+BLS_INL fp lds_ld(const uint32_t* b, int q) {
+  fp r;
+#pragma unroll
+  for (int l = 0; l < BLS_NL; l++) r.l[l] = b[q * BLS_NL + l];
+  return r;
+}
+BLS_INL void lds_st(uint32_t* b, int q, const fp& v) {
+#pragma unroll
+  for (int l = 0; l < BLS_NL; l++) b[q * BLS_NL + l] = v.l[l];
+}
+
+// (x0 + x1 u)^2 = (x0 + x1)(x0 - x1) + (2 x0) x1 u : operands of component `comp`'s single product.  x0, x1:
+// normalized limbs, values <= 4p; the operands are lazy (limbs < 2^30, values < 12p: fp_mul's contract)
+BLS_INL void sqr_operands(const fp& x0, const fp& x1, int comp, fp& X, fp& Y) {
+  X = comp ? fp_add_nr(x0, x0) : fp_add_nr(x0, x1);
+  Y = comp ? x1 : fp_sub_k8(x0, x1);
+}
+// Karatsuba component c of (a0 + a1 u)(b0 + b1 u): c0 = a0 b0, c1 = a1 b1, c2 = (a0 + a1)(b0 + b1)
+BLS_INL void kara_operands(const fp& a0, const fp& a1, const fp& b0, const fp& b1, int c, fp& X, fp& Y) {
+  X = c == 0 ? a0 : (c == 1 ? a1 : fp_add_nr(a0, a1));
+  Y = c == 0 ? b0 : (c == 1 ? b1 : fp_add_nr(b0, b1));
+}
+

@@ -686,7 +686,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     HIPCHK(hipStreamWaitEvent(sp, sl.join_in, 0));
     // messages
     beg(1, sm);
-    launch_hash_to_g2(pb, sm);
+    launch_hash_to_g2(pb, sm, coop);
     launch_h_affine(pb, sm);
     end(1, sm);
     beg(kStages, sm);
@@ -703,7 +703,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     HIPCHK(hipEventRecord(sl.join_pk, sp));
     // signatures, then the batch equation
     beg(0, s);
-    launch_sig_decode(pb, n, s);
+    launch_sig_decode(pb, n, s, coop);
     end(0, s);
     HIPCHK(hipStreamWaitEvent(s, sl.join_pk, 0));
     beg(4, s);

@@ -5,6 +5,7 @@
 #include "../../lodestar_amd/csrc/ops.hpp"
 #include "../../lodestar_amd/csrc/msm.hpp"
 #include "../../lodestar_amd/csrc/lacc.hpp"
+#include "../../lodestar_amd/csrc/g2_coop.hpp"
 
 #if defined(BLS_COUNT_OPS)
 unsigned long long bls_count_mul = 0, bls_count_sqr = 0, bls_count_half = 0;
@@ -141,6 +142,15 @@ void emu_sqr_operands_mul(const uint32_t* x0, const uint32_t* x1, uint32_t* out1
   }
   const fp r = fp_mul(fp_add_nr(a, b), fp_sub_k8(a, b));
   for (int i = 0; i < BLS_NL; i++) out14[i] = r.l[i];
+}
+// the cooperative doubling chain (g2_coop.hpp, phases run lane by lane): [|z|]P for an affine P
+int emu_g2c_mul_zabs(const uint8_t* p192, uint8_t* out192) {
+  const g2a a = load_g2(p192);
+  const g2j r = g2c_host_mul_zabs(jac_from_aff(a), [&] { return jac_from_aff(a); });
+  g2a o;
+  if (!jac_to_aff(r, o)) return 0;
+  g2a_to_be192(o, out192);
+  return 1;
 }
 #if defined(BLS_COUNT_OPS)
 // bucket MSM over n distinct points (the count covers the MSM only, not the point loads)

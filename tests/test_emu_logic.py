@@ -364,3 +364,21 @@ def test_lacc_fin_and_lazy_operands():
         v = _val(out)
         assert all(x < 2**28 for x in out[:13]) and v < 2 * P, trial
         assert v % P == (x0 + x1) * (x0 - x1) * R_INV % P, trial
+
+
+def test_cooperative_g2_doubling_chain():
+    """g2_coop.hpp: the [|z|] chain as the 16-lane groups run it (three product phases + two recombinations per
+    doubling, additions on lane 0), phases executed lane by lane on the host, against the oracle's [|z|]P -- on G2
+    points and on points of E2 outside G2 (the cofactor clearing's inputs)."""
+    L = lib()
+    o = buf(192)
+    r2 = random.Random(808)
+    pts = [bls.g2_mul(bls.G2_GEN, r2.randrange(1, bls.R)) for _ in range(3)]
+    while len(pts) < 6:  # points of E2 not in G2
+        x = (r2.randrange(P), r2.randrange(P))
+        y = bls.f2sqrt(bls.f2add(bls.f2mul(bls.f2sqr(x), x), bls.B2))
+        if y:
+            pts.append((x, y))
+    for q in pts:
+        assert L.emu_g2c_mul_zabs(g2b(q), o) == 1
+        assert b2g2(o.raw) == bls.g2_mul(q, 0xD201000000010000)

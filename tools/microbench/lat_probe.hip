@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include "../../lodestar_amd/csrc/gt_wave.hpp"
+#include "../../lodestar_amd/csrc/g2_coop.hpp"
 
 #define CHECK(x)                                                                   \
   do {                                                                             \
@@ -17,17 +18,18 @@
   } while (0)
 
 enum { P_MUL, P_SQR, P_FP2MUL, P_INV, P_INVPOW, P_POW34, P_G2DBL, P_CYC, P_GMUL, P_GSPARSE, P_FINEXP, P_FP12INV, P_CYC1,
-       P_CYC2, P_SYNC, P_LACC, NP };
+       P_CYC2, P_SYNC, P_LACC, P_G2C, P_G2C_P1, P_G2C_R1, NP };
 static const char* NAMES[NP] = {"fp_mul", "fp_sqr", "fp2_mul", "fp_inv_divsteps", "fp_inv_pow", "fp_pow_p34",
                                 "g2_jac_dbl", "gtw_cyc_sqr", "gtw_mul", "gtw_mul_sparse", "gtw_final_exp",
                                 "fp12_inv_lane0", "gtw_cyc_sqr_products", "gtw_cyc_sqr_recombine", "gtw_sync",
-                                "lacc_fin_lane"};
-static const int REPS[NP] = {256, 256, 128, 8, 4, 4, 32, 64, 32, 32, 1, 2, 64, 64, 256, 256};
+                                "lacc_fin_lane", "g2c_dbl", "g2c_dbl_p1", "g2c_dbl_r1"};
+static const int REPS[NP] = {256, 256, 128, 8, 4, 4, 32, 64, 32, 32, 1, 2, 64, 64, 256, 256, 64, 64, 64};
 
 __device__ __forceinline__ uint64_t now() { return wall_clock64(); }
 
 __global__ __launch_bounds__(GTW_LANES) void k_probe(uint64_t* ticks, uint32_t seed, uint32_t* sink) {
   __shared__ GtwLds sh;
+  __shared__ uint32_t g2lds[(GTW_LANES / G2C_LANES) * G2C_WORDS];
   const uint32_t t = threadIdx.x;
   fp a, b;
   for (int i = 0; i < BLS_NL; i++) {
@@ -37,6 +39,7 @@ __global__ __launch_bounds__(GTW_LANES) void k_probe(uint64_t* ticks, uint32_t s
   a.l[BLS_NL - 1] &= 0xffff;
   b.l[BLS_NL - 1] &= 0xffff;
   // Fp12 values in LDS
+  for (uint32_t w = t; w < (GTW_LANES / G2C_LANES) * G2C_WORDS; w += GTW_LANES) g2lds[w] = (seed * 7 + 11 * w) & 0xFFFFFFu;
   for (uint32_t w = t; w < 12 * BLS_NL; w += GTW_LANES) {
     sh.F[w] = (seed + 31 * w) & BLS_MASK;
     sh.G[w] = (seed * 3 + 17 * w) & BLS_MASK;
@@ -64,6 +67,9 @@ __global__ __launch_bounds__(GTW_LANES) void k_probe(uint64_t* ticks, uint32_t s
         case P_CYC1: gtw_cyc_sqr<1>(sh.F, sh.F, sh.S, t); break;
         case P_CYC2: gtw_cyc_sqr<2>(sh.F, sh.F, sh.S, t); break;
         case P_SYNC: gtw_sync(); break;
+        case P_G2C: g2c_dbl(g2lds + (t / G2C_LANES) * G2C_WORDS, t % G2C_LANES); break;
+        case P_G2C_P1: g2c_dbl_p1(g2lds + (t / G2C_LANES) * G2C_WORDS, t % G2C_LANES); gtw_sync(); break;
+        case P_G2C_R1: g2c_dbl_r1(g2lds + (t / G2C_LANES) * G2C_WORDS, t % G2C_LANES); gtw_sync(); break;
         case P_LACC: if (t == 0) { lacc q; for (int i = 0; i < BLS_NL; i++) { q.pos[i] = a.l[i]; q.neg[i] = b.l[i]; } a = lacc_fin(q); } break;
       }
     }
