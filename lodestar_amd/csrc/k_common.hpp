@@ -6,6 +6,12 @@
 #include "ops.hpp"
 
 #define WAVE 64
+#if defined(__HIP_DEVICE_COMPILE__) && !BLS_INLINE_PRODUCTS && !BLS_FP2_CLASSIC
+// fp2_mul's LDS argument slot is indexed by threadIdx.x: every launch shape of the kernels stays within it
+// (BLSGPU_DEBUG=1 builds also assert it at run time, tower.hpp)
+static_assert(WAVE <= BLS_FP2_LDS_LANES, "fp2_mul LDS slot");
+static_assert(2 * WAVE <= BLS_FP2_LDS_LANES, "128-lane kernels (gt_wave.hpp, k_msm_bucket) and fp2_mul LDS slot");
+#endif
 
 // Lane-per-set stage kernels.  BLSGPU_WPE is the number of waves per SIMD the register budget is sized for:
 // 1 lets a kernel take the whole 512-entry VGPR+AGPR file (no spills, but one resident wave per SIMD, so

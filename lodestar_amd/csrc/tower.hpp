@@ -105,6 +105,9 @@ BLS_INL fp2 fp2_sqr_body(const fp2& a) {
 // SIMD with this call vs 1.39e10 for three fp_mul_r calls.
 #if defined(__HIP_DEVICE_COMPILE__) && !BLS_INLINE_PRODUCTS && !BLS_FP2_CLASSIC
 #define BLS_FP2_LDS_LANES 128
+#if BLSGPU_DEBUG
+#include <assert.h>
+#endif
 __shared__ uint32_t bls_fp2_arg[2 * BLS_NL * BLS_FP2_LDS_LANES];
 // The 28-dword result comes back in VGPRs as a 32-wide vector: clang's AMDGPU ABI returns an aggregate of more than
 // 16 dwords indirectly (through a scratch sret slot: 7 dwordx4 stores + 7 loads per call), a vector type directly.
@@ -148,6 +151,10 @@ __device__ __forceinline__ fp2 fp2_from_ret(const fp2_ret& o) {
 }
 __device__ __forceinline__ fp2 fp2_mul(const fp2& a, const fp2& b) {
   const uint32_t t = threadIdx.x;
+#if BLSGPU_DEBUG
+  // the slot is indexed by threadIdx.x alone: one-dimensional workgroups of <= 128 lanes only
+  assert(blockDim.x <= BLS_FP2_LDS_LANES && blockDim.y == 1 && blockDim.z == 1);
+#endif
 #pragma unroll
   for (int i = 0; i < BLS_NL; i++) {
     bls_fp2_arg[i * BLS_FP2_LDS_LANES + t] = b.c0.l[i];
@@ -174,6 +181,9 @@ __device__ __noinline__ fp2_ret fp2_mul_fp_r(BLS_PARAMS14(a), BLS_PARAMS14(c)) {
 }
 __device__ __forceinline__ fp2 fp2_mul_fp(const fp2& a, const fp& s) {
   const uint32_t t = threadIdx.x;
+#if BLSGPU_DEBUG
+  assert(blockDim.x <= BLS_FP2_LDS_LANES && blockDim.y == 1 && blockDim.z == 1);
+#endif
 #pragma unroll
   for (int i = 0; i < BLS_NL; i++) bls_fp2_arg[i * BLS_FP2_LDS_LANES + t] = s.l[i];
   return fp2_from_ret(fp2_mul_fp_r(BLS_ARGS14(a.c0), BLS_ARGS14(a.c1)));
