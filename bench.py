@@ -460,6 +460,8 @@ def main():
     ap.add_argument("--pipeline-depth", type=int, default=None, help="runs in flight per device (runtime default 2)")
     ap.add_argument("--merge-wait-us", type=int, default=None,
                     help="how long a slot lingers for more calls to merge while runs are in flight (runtime default)")
+    ap.add_argument("--idle-wait-us", type=int, default=None,
+                    help="on an idle device, how long a slot waits while a burst of calls keeps arriving (runtime default)")
     ap.add_argument("--miller-k", type=int, default=0,
                     help="pairings per Miller accumulator (shared squarings); 0 = the runtime's choice by run size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -496,6 +498,8 @@ def main():
         ctx.set_option("pipeline_depth", args.pipeline_depth)
     if args.merge_wait_us is not None:
         ctx.set_option("merge_wait_us", args.merge_wait_us)
+    if args.idle_wait_us is not None:
+        ctx.set_option("idle_wait_us", args.idle_wait_us)
     work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev)
     expected = work.pop("expected", None)
     if expected is None:
@@ -583,7 +587,8 @@ def main():
                        batch_groups_per_step=groups, inflight=args.inflight,
                        slots=ctx.get_option("slots"), hw_queues=ctx.get_option("hw_queues"),
                        merge_sets=args.merge_sets, pipeline_depth=ctx.get_option("pipeline_depth"),
-                       merge_wait_us=ctx.get_option("merge_wait_us"), pipeline_runs_timed=len(runs_timed),
+                       merge_wait_us=ctx.get_option("merge_wait_us"), idle_wait_us=ctx.get_option("idle_wait_us"),
+                       pipeline_runs_timed=len(runs_timed),
                        parallelism=f"shard-by-job x{n_gpus} ({'one process per GPU' if world > 1 else 'in-process devices'}), no collective"),
         "p50_batch_latency_ms": round(float(np.median(lat)), 3),
         "call_latency_under_load_ms": {"p50": round(float(np.percentile(call_lat, 50)), 2),

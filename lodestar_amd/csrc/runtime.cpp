@@ -192,6 +192,7 @@ struct Options {  // snapshot taken at the start of each call
   int64_t miller_k = 0;  // pairings per Miller accumulator (shared squarings); 0 = by run size (miller_k_auto)
   int64_t merge_sets = 131072;  // queued calls a slot merges into one pipeline run (sets), 0 = never
   int64_t merge_wait_us = 2000;  // while runs are in flight, a slot waits this long for more calls to merge
+  int64_t idle_wait_us = 0;  // on an idle device, a slot waits up to this long while calls keep arriving (bursts)
   int64_t pipeline_depth = 3;    // runs a device has in flight (taken by a slot, batch pass not yet complete)
   int64_t group_policy = 0;    // 0 = groups of >= group_sets sets; 1 = the reference pool's jobs / requests / chunks
   bool same_run(const struct Options& o) const {
@@ -1322,8 +1323,14 @@ void worker_loop(Device* d, Slot* sl) {
       const Call* c0 = parts[0].call;
       uint32_t total = task_sets(parts[0]);
       const int64_t cap = c0->opt.merge_sets;
-      const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(c0->opt.merge_wait_us);
+      const auto t_start = std::chrono::steady_clock::now();
+      const auto deadline = t_start + std::chrono::microseconds(c0->opt.merge_wait_us);
+      // idle device: linger only while a burst keeps arriving -- each new call extends the wait by idle_wait_us / 4,
+      // up to idle_wait_us in all, so an isolated call waits at most idle_wait_us / 4
+      const auto idle_end = t_start + std::chrono::microseconds(c0->opt.idle_wait_us);
+      auto idle_deadline = t_start + std::chrono::microseconds(c0->opt.idle_wait_us / 4);
       for (;;) {
+        size_t took = 0;
         while (!d->queue.empty() && cap > 0 && !(c0->ctx->closed)) {
           const Task& nx = d->queue.front();
           const Call* c = nx.call;
@@ -1332,9 +1339,18 @@ void worker_loop(Device* d, Slot* sl) {
           total += task_sets(nx);
           parts.push_back(nx);
           d->queue.pop_front();
+          took++;
         }
         const bool room = cap > 0 && (int64_t)total < cap && d->queue.empty();
-        if (!room || d->runs_inflight == 0 || d->stop || c0->ctx->closed) break;
+        if (!room || d->stop || c0->ctx->closed) break;
+        if (d->runs_inflight == 0) {
+          if (c0->opt.idle_wait_us <= 0) break;
+          const auto now = std::chrono::steady_clock::now();
+          if (took) idle_deadline = std::min(idle_end, now + std::chrono::microseconds(c0->opt.idle_wait_us / 4));
+          if (now >= idle_deadline) break;
+          if (d->q_cv.wait_until(lk, idle_deadline) == std::cv_status::timeout && d->queue.empty()) break;
+          continue;
+        }
         if (d->q_cv.wait_until(lk, deadline) == std::cv_status::timeout && d->queue.empty()) break;
       }
       d->runs_inflight++;
@@ -1682,6 +1698,9 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "merge_wait_us") {
     if (value < 0 || value > 1000000) return BLSGPU_ERR_ARGS;
     ctx->opt.merge_wait_us = value;
+  } else if (k == "idle_wait_us") {
+    if (value < 0 || value > 1000000) return BLSGPU_ERR_ARGS;
+    ctx->opt.idle_wait_us = value;
   } else if (k == "pipeline_depth") {
     if (value < 1 || value > 64) return BLSGPU_ERR_ARGS;
     ctx->opt.pipeline_depth = value;
@@ -1723,6 +1742,7 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "miller_k") *value = o.miller_k;
   else if (k == "group_policy") *value = o.group_policy;
   else if (k == "merge_wait_us") *value = o.merge_wait_us;
+  else if (k == "idle_wait_us") *value = o.idle_wait_us;
   else if (k == "pipeline_depth") *value = o.pipeline_depth;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
