@@ -20,29 +20,35 @@ BLS_CONST uint32_t SHA256_IV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53
 
 BLS_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
-// One compression of a 16-word (big-endian words) block into state st.
-BLS_HDNI void sha256_block(uint32_t st[8], const uint32_t blk[16]) {
+// One compression of a 16-word (big-endian words) block into the state.  State and block travel by value as
+// aggregates of <= 16 dwords, which the AMDGPU calling convention passes and returns in VGPRs; the schedule is fully
+// unrolled, so w[] is register-resident too (no scratch frame).
+struct sha_st {
+  uint32_t h[8];
+};
+struct sha_blk {
   uint32_t w[16];
-  for (int i = 0; i < 16; i++) w[i] = blk[i];
-  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll 16
+};
+BLS_HDNI sha_st sha256_block(sha_st st, sha_blk blk) {
+  uint32_t a = st.h[0], b = st.h[1], c = st.h[2], d = st.h[3], e = st.h[4], f = st.h[5], g = st.h[6], h = st.h[7];
+#pragma unroll
   for (int i = 0; i < 64; i++) {
     uint32_t wi;
     if (i < 16) {
-      wi = w[i & 15];
+      wi = blk.w[i];
     } else {
-      uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-      uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
-      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-      w[i & 15] = wi;
+      const uint32_t w15 = blk.w[(i - 15) & 15], w2 = blk.w[(i - 2) & 15];
+      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      wi = blk.w[i & 15] + s0 + blk.w[(i - 7) & 15] + s1;
+      blk.w[i & 15] = wi;
     }
-    uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
-    uint32_t ch = (e & f) ^ (~e & g);
-    uint32_t t1 = h + S1 + ch + SHA256_K[i] + wi;
-    uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-    uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
-    uint32_t t2 = S0 + maj;
+    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = h + S1 + ch + SHA256_K[i] + wi;
+    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t t2 = S0 + maj;
     h = g;
     g = f;
     f = e;
@@ -52,66 +58,83 @@ BLS_HDNI void sha256_block(uint32_t st[8], const uint32_t blk[16]) {
     b = a;
     a = t1 + t2;
   }
-  st[0] += a;
-  st[1] += b;
-  st[2] += c;
-  st[3] += d;
-  st[4] += e;
-  st[5] += f;
-  st[6] += g;
-  st[7] += h;
+  st.h[0] += a;
+  st.h[1] += b;
+  st.h[2] += c;
+  st.h[3] += d;
+  st.h[4] += e;
+  st.h[5] += f;
+  st.h[6] += g;
+  st.h[7] += h;
+  return st;
 }
 
-// Byte-wise writer into a word buffer (big-endian words)
+// Byte-wise writer into a word buffer (big-endian words); every call site has a constant position
 BLS_HD void put_byte(uint32_t* words, int pos, uint32_t byte) {
   words[pos >> 2] |= (byte & 0xffu) << (24 - 8 * (pos & 3));
 }
+BLS_INL sha_blk sha_blk_of(const uint32_t* w) {
+  sha_blk b;
+#pragma unroll
+  for (int i = 0; i < 16; i++) b.w[i] = w[i];
+  return b;
+}
 
-// expand_message_xmd(msg(32), DST, 256) -> 64 words (big-endian)
-BLS_HDNI void expand_message_xmd_32(const uint8_t msg[32], uint32_t out[64]) {
+// expand_message_xmd(msg(32), DST, 256) -> 64 words (big-endian).  Inlined with every loop unrolled: all buffer
+// positions are constants, so the buffers live in registers.
+BLS_INL void expand_message_xmd_32(const uint8_t msg[32], uint32_t out[64]) {
   // b0 = H(Z_pad(64) || msg || I2OSP(256,2) || 0x00 || DST || len(DST))
   // Z_pad fills exactly the first block: start from the state after compressing a zero block.
-  uint32_t st[8];
-  for (int i = 0; i < 8; i++) st[i] = SHA256_IV[i];
-  uint32_t blk[16];
-  for (int i = 0; i < 16; i++) blk[i] = 0;
-  sha256_block(st, blk);
+  sha_st st;
+#pragma unroll
+  for (int i = 0; i < 8; i++) st.h[i] = SHA256_IV[i];
+  sha_blk zero;
+#pragma unroll
+  for (int i = 0; i < 16; i++) zero.w[i] = 0;
+  st = sha256_block(st, zero);
   // remaining bytes: msg(32) || 0x01 0x00 || 0x00 || DST(43) || 43  = 79 bytes, total 143
   uint32_t buf[32];
+#pragma unroll
   for (int i = 0; i < 32; i++) buf[i] = 0;
-  int pos = 0;
-  for (int i = 0; i < 32; i++) put_byte(buf, pos++, msg[i]);
-  put_byte(buf, pos++, 0x01);
-  put_byte(buf, pos++, 0x00);
-  put_byte(buf, pos++, 0x00);
-  for (int i = 0; i < BLS_DST_LEN; i++) put_byte(buf, pos++, BLS_DST[i]);
-  put_byte(buf, pos++, BLS_DST_LEN);
-  put_byte(buf, pos++, 0x80);
+#pragma unroll
+  for (int i = 0; i < 32; i++) put_byte(buf, i, msg[i]);
+  put_byte(buf, 32, 0x01);
+  put_byte(buf, 33, 0x00);
+  put_byte(buf, 34, 0x00);
+#pragma unroll
+  for (int i = 0; i < BLS_DST_LEN; i++) put_byte(buf, 35 + i, BLS_DST[i]);
+  put_byte(buf, 35 + BLS_DST_LEN, BLS_DST_LEN);
+  put_byte(buf, 36 + BLS_DST_LEN, 0x80);
   // total length 143 bytes = 1144 bits, in the last 8 bytes of the second block of buf
   buf[31] = 143u * 8u;
-  sha256_block(st, buf);
-  sha256_block(st, buf + 16);
-  uint32_t b0[8];
-  for (int i = 0; i < 8; i++) b0[i] = st[i];
+  st = sha256_block(st, sha_blk_of(buf));
+  st = sha256_block(st, sha_blk_of(buf + 16));
+  const sha_st b0 = st;
   // b_i = H((b0 ^ b_{i-1}) || I2OSP(i,1) || DST || len(DST)) : 32 + 1 + 44 = 77 bytes -> 2 blocks
-  uint32_t prev[8];
-  for (int i = 0; i < 8; i++) prev[i] = 0;
+  sha_st prev;
+#pragma unroll
+  for (int i = 0; i < 8; i++) prev.h[i] = 0;
+#pragma unroll
   for (int idx = 1; idx <= 8; idx++) {
-    for (int i = 0; i < 32; i++) buf[i] = 0;
-    for (int i = 0; i < 8; i++) buf[i] = (idx == 1) ? b0[i] : (b0[i] ^ prev[i]);
-    pos = 32;
-    put_byte(buf, pos++, (uint32_t)idx);
-    for (int i = 0; i < BLS_DST_LEN; i++) put_byte(buf, pos++, BLS_DST[i]);
-    put_byte(buf, pos++, BLS_DST_LEN);
-    put_byte(buf, pos++, 0x80);
-    buf[31] = 77u * 8u;
-    for (int i = 0; i < 8; i++) st[i] = SHA256_IV[i];
-    sha256_block(st, buf);
-    sha256_block(st, buf + 16);
-    for (int i = 0; i < 8; i++) {
-      prev[i] = st[i];
-      out[(idx - 1) * 8 + i] = st[i];
-    }
+    uint32_t bb[32];
+#pragma unroll
+    for (int i = 0; i < 32; i++) bb[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) bb[i] = b0.h[i] ^ prev.h[i];
+    put_byte(bb, 32, (uint32_t)idx);
+#pragma unroll
+    for (int i = 0; i < BLS_DST_LEN; i++) put_byte(bb, 33 + i, BLS_DST[i]);
+    put_byte(bb, 33 + BLS_DST_LEN, BLS_DST_LEN);
+    put_byte(bb, 34 + BLS_DST_LEN, 0x80);
+    bb[31] = 77u * 8u;
+    sha_st s2;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s2.h[i] = SHA256_IV[i];
+    s2 = sha256_block(s2, sha_blk_of(bb));
+    s2 = sha256_block(s2, sha_blk_of(bb + 16));
+#pragma unroll
+    for (int i = 0; i < 8; i++) out[(idx - 1) * 8 + i] = s2.h[i];
+    prev = s2;
   }
 }
 
@@ -140,7 +163,7 @@ BLS_HD fp fp_from_be64_words(const uint32_t* w) {
 }
 
 // hash_to_field(msg, 2) -> u0, u1 in Fp2
-BLS_HDNI void hash_to_field_fp2x2(const uint8_t msg[32], fp2& u0, fp2& u1) {
+BLS_INL void hash_to_field_fp2x2(const uint8_t msg[32], fp2& u0, fp2& u1) {
   uint32_t ub[64];
   expand_message_xmd_32(msg, ub);
   u0.c0 = fp_from_be64_words(ub + 0);
@@ -151,7 +174,7 @@ BLS_HDNI void hash_to_field_fp2x2(const uint8_t msg[32], fp2& u0, fp2& u1) {
 
 // ----------------------------------------------------------------------------- sqrt helpers
 // Given a in Fp2 and s = a square root of N(a) (in Fp), return a square root of a (if a is a square).
-BLS_HDNI fp2 fp2_sqrt_with_normroot(const fp2& a, const fp& s) {
+BLS_INL fp2 fp2_sqrt_with_normroot(const fp2& a, const fp& s) {
   fp t = fp_half(fp_add(a.c0, s));
   fp t_alt = fp_half(fp_sub(a.c0, s));
   t = fp_select(fp_is_zero(t), t_alt, t);
@@ -171,7 +194,7 @@ BLS_HD fp2 fp2_plain(const fp2& a) { return fp2_make(fp_from_mont(a.c0), fp_from
 // ----------------------------------------------------------------------------- SSWU + iso3
 // map_to_curve_simple_swu on E2': y^2 = x^3 + A'x + B'.  `tv_inv` = inv0(Z^2 u^4 + Z u^2) supplied by
 // the caller (batched with the other map's inversion).
-BLS_HDNI g2a sswu_map(const fp2& u, const fp2& Zu2, const fp2& tv, const fp2& tv_inv) {
+BLS_INL g2a sswu_map(const fp2& u, const fp2& Zu2, const fp2& tv, const fp2& tv_inv) {
   fp2 x1 = fp2_mul(SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), tv_inv));
   x1 = fp2_select(fp2_is_zero(tv), SSWU_B_OVER_ZA, x1);
   fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), SSWU_A), x1), SSWU_B);
@@ -199,7 +222,7 @@ BLS_HDNI g2a sswu_map(const fp2& u, const fp2& Zu2, const fp2& tv, const fp2& tv
 
 // 3-isogeny E2' -> E2 producing a Jacobian point (no inversion):
 //   x = Nx/Dx, y = y' Ny/Dy  ->  Z = Dx Dy, X = Nx Dx Dy^2, Y = y' Ny Dx^3 Dy^2
-BLS_HDNI g2j iso3_map_jac(const g2a& p) {
+BLS_INL g2j iso3_map_jac(const g2a& p) {
   const fp2& x = p.x;
   fp2 x2 = fp2_sqr(x);
   fp2 x3 = fp2_mul(x2, x);
@@ -235,7 +258,7 @@ BLS_HDNI g2j clear_cofactor_g2(const g2j& P) {
 // instead of registers, reordered so that only the accumulator is live across each [|z|] chain:
 //   A = [|z|]P,   C = psi^2(2P) - psi(P) + A - P,   D = [|z|](A - psi(P)),   h_eff P = C + D
 // (clear_cofactor_g2's t3 + t2 - t1 - P with t1 = -A, t2 = D, t3 = psi^2(2P) - psi(P)).  Slot 0 holds P on entry;
-// slots 1 and 2 are overwritten.
+// slots 1 and 2 are overwritten.  Slot 1 may be slot 0 itself (P is in registers before slot 1 is written).
 template <class Ld, class St>
 BLS_INL g2j clear_cofactor_g2_slots(Ld ld, St st) {
   const g2j A = jac_mul_zabs_ld<fp2>([&] { return ld(0); });
@@ -257,7 +280,7 @@ BLS_INL g2j clear_cofactor_g2_slots(Ld ld, St st) {
 struct h2c_prep {
   fp2 u0, u1, Zu2_0, Zu2_1, tv0, tv1, d;
 };
-BLS_HDNI void hash_to_g2_prep(const uint8_t msg[32], h2c_prep& h) {
+BLS_INL void hash_to_g2_prep(const uint8_t msg[32], h2c_prep& h) {
   hash_to_field_fp2x2(msg, h.u0, h.u1);
   h.Zu2_0 = fp2_mul(SSWU_Z, fp2_sqr(h.u0));
   h.Zu2_1 = fp2_mul(SSWU_Z, fp2_sqr(h.u1));
@@ -269,7 +292,7 @@ BLS_HDNI void hash_to_g2_prep(const uint8_t msg[32], h2c_prep& h) {
 }
 // One of the two maps (j = 0, 1) of the finish step: iso3(SSWU(u_j)) as a Jacobian point.  The pipeline runs the
 // two maps of a message on two lanes (k_hash_map), then sums and clears the cofactor (k_hash_clear).
-BLS_HDNI g2j hash_to_g2_map_j(const h2c_prep& h, const fp2& dinv, int j) {
+BLS_INL g2j hash_to_g2_map_j(const h2c_prep& h, const fp2& dinv, int j) {
   const bool z0 = fp2_is_zero(h.tv0), z1 = fp2_is_zero(h.tv1);
   const fp2 a_other = j == 0 ? fp2_select(z1, fp2_one(), h.tv1) : fp2_select(z0, fp2_one(), h.tv0);
   const bool zj = j == 0 ? z0 : z1;

@@ -59,23 +59,22 @@ STAGE_KERNEL_W(BLSGPU_WPE_HMAP) void k_hash_map(PipelineBuffers b, const uint32_
 }
 
 // Q = q0 + q1, cofactor clearing (RFC 9380 G.3); Jacobian out + N(z) for the batched affine conversion.  The
-// clearing keeps its intermediate points in this lane's own SoA slots (clear_cofactor_g2_slots): slot 0 = h_q[2u]
-// (q0, then Q), slot 1 = h_q[2u + 1] (q1, then A - psi(Q)), slot 2 = h_jac[u] (C, then the result).
+// clearing (clear_cofactor_g2_slots) keeps the base point of each [|z|] chain -- Q, then A - psi(Q) -- in this lane's
+// LDS slot (word-major, conflict-free), re-read at the chain's five additions, and C in h_jac[u] until the end: no
+// point stays in registers across a chain, and the re-reads never reach HBM.
 STAGE_KERNEL_W(BLSGPU_WPE_HASH) void k_hash_clear(PipelineBuffers b) {
+  __shared__ uint32_t base[W_G2J * WAVE];
   const uint32_t u = blockIdx.x * WAVE + threadIdx.x;
   if (u >= b.n_umsg) return;
-  const uint32_t qs = 2 * b.nm;
-  st_g2j(b.h_q, qs, 2 * u, jac_add(ld_g2j(b.h_q, qs, 2 * u), ld_g2j(b.h_q, qs, 2 * u + 1)));
+  const uint32_t qs = 2 * b.nm, t = threadIdx.x;
+  st_g2j(base, WAVE, t, jac_add(ld_g2j(b.h_q, qs, 2 * u), ld_g2j(b.h_q, qs, 2 * u + 1)));
   const g2j H = clear_cofactor_g2_slots(
-      [&](int k) {
-        const uint32_t v = opaque_u32(u);
-        return k == 2 ? ld_g2j(b.h_jac, b.nm, v) : ld_g2j(b.h_q, qs, 2 * v + k);
-      },
+      [&](int k) { return k == 2 ? ld_g2j(b.h_jac, b.nm, u) : ld_g2j(base, WAVE, opaque_u32(t)); },
       [&](int k, const g2j& v) {
         if (k == 2)
           st_g2j(b.h_jac, b.nm, u, v);
         else
-          st_g2j(b.h_q, qs, 2 * u + k, v);
+          st_g2j(base, WAVE, t, v);  // slot 1 (A - psi Q) replaces slot 0 (Q): read into registers before
       });
   st_g2j(b.h_jac, b.nm, u, H);
   st_fp(b.h_norm, b.nm, u, 0, fp2_norm(H.z));

@@ -6,18 +6,18 @@
 
 // SHA-256 of a 64-byte message given as 16 big-endian words -> 8 state words
 __device__ void sha256_64(const uint32_t in[16], uint32_t out[8]) {
-  uint32_t st[8];
+  sha_st st;
 #pragma unroll
-  for (int i = 0; i < 8; i++) st[i] = SHA256_IV[i];
-  sha256_block(st, in);
-  uint32_t pad[16];
+  for (int i = 0; i < 8; i++) st.h[i] = SHA256_IV[i];
+  st = sha256_block(st, sha_blk_of(in));
+  sha_blk pad;
 #pragma unroll
-  for (int i = 0; i < 16; i++) pad[i] = 0;
-  pad[0] = 0x80000000u;
-  pad[15] = 512u;
-  sha256_block(st, pad);
+  for (int i = 0; i < 16; i++) pad.w[i] = 0;
+  pad.w[0] = 0x80000000u;
+  pad.w[15] = 512u;
+  st = sha256_block(st, pad);
 #pragma unroll
-  for (int i = 0; i < 8; i++) out[i] = st[i];
+  for (int i = 0; i < 8; i++) out[i] = st.h[i];
 }
 
 __device__ __forceinline__ uint32_t be32(const uint8_t* p) {

@@ -376,9 +376,10 @@ extern "C" int emu_hash_to_g2_split(const uint8_t* msg, uint8_t* out192) {
   h2c_prep h;
   hash_to_g2_prep(msg, h);
   const fp2 dinv = fp2_inv(h.d);
-  g2j slot[3];
+  g2j slot[2];  // as k_hash_clear: slots 0 and 1 share one place (the LDS base point), slot 2 its own
   slot[0] = jac_add(hash_to_g2_map_j(h, dinv, 0), hash_to_g2_map_j(h, dinv, 1));
-  const g2j H = clear_cofactor_g2_slots([&](int k) { return slot[k]; }, [&](int k, const g2j& v) { slot[k] = v; });
+  const g2j H = clear_cofactor_g2_slots([&](int k) { return slot[k == 2 ? 1 : 0]; },
+                                        [&](int k, const g2j& v) { slot[k == 2 ? 1 : 0] = v; });
   g2a a;
   if (!jac_to_aff(H, a)) return 0;
   g2a_to_be192(a, out192);

@@ -18,12 +18,13 @@
   } while (0)
 
 enum { P_MUL, P_SQR, P_FP2MUL, P_INV, P_INVPOW, P_POW34, P_G2DBL, P_CYC, P_GMUL, P_GSPARSE, P_FINEXP, P_FP12INV, P_CYC1,
-       P_CYC2, P_SYNC, P_LACC, P_G2C, P_G2C_P1, P_G2C_R1, NP };
+       P_CYC2, P_SYNC, P_LACC, P_G2C, P_G2C_P1, P_G2C_R1, P_G2ADD, P_G2ADDAFF, P_MILLER, P_FP12MUL, NP };
 static const char* NAMES[NP] = {"fp_mul", "fp_sqr", "fp2_mul", "fp_inv_divsteps", "fp_inv_pow", "fp_pow_p34",
                                 "g2_jac_dbl", "gtw_cyc_sqr", "gtw_mul", "gtw_mul_sparse", "gtw_final_exp",
                                 "fp12_inv_lane0", "gtw_cyc_sqr_products", "gtw_cyc_sqr_recombine", "gtw_sync",
-                                "lacc_fin_lane", "g2c_dbl", "g2c_dbl_p1", "g2c_dbl_r1"};
-static const int REPS[NP] = {256, 256, 128, 8, 4, 4, 32, 64, 32, 32, 1, 2, 64, 64, 256, 256, 64, 64, 64};
+                                "lacc_fin_lane", "g2c_dbl", "g2c_dbl_p1", "g2c_dbl_r1", "g2_jac_add", "g2_jac_add_aff",
+                                "gtw_miller_loop", "fp12_mul_lane"};
+static const int REPS[NP] = {256, 256, 128, 8, 4, 4, 32, 64, 32, 32, 1, 2, 64, 64, 256, 256, 64, 64, 64, 16, 16, 1, 16};
 
 __device__ __forceinline__ uint64_t now() { return wall_clock64(); }
 
@@ -70,6 +71,10 @@ __global__ __launch_bounds__(GTW_LANES) void k_probe(uint64_t* ticks, uint32_t s
         case P_G2C: g2c_dbl(g2lds + (t / G2C_LANES) * G2C_WORDS, t % G2C_LANES); break;
         case P_G2C_P1: g2c_dbl_p1(g2lds + (t / G2C_LANES) * G2C_WORDS, t % G2C_LANES); gtw_sync(); break;
         case P_G2C_R1: g2c_dbl_r1(g2lds + (t / G2C_LANES) * G2C_WORDS, t % G2C_LANES); gtw_sync(); break;
+        case P_G2ADD: if (t == 0) { g2j q, r; q.x = fp2_make(a, b); q.y = fp2_make(b, a); q.z = fp2_make(a, a); r.x = fp2_make(b, b); r.y = fp2_make(a, b); r.z = fp2_make(b, a); q = jac_add(q, r); a = q.x.c0; b = q.y.c1; } break;
+        case P_G2ADDAFF: if (t == 0) { g2j q; g2a r; q.x = fp2_make(a, b); q.y = fp2_make(b, a); q.z = fp2_make(a, a); r.x = fp2_make(b, b); r.y = fp2_make(a, b); q = jac_add_aff(q, r); a = q.x.c0; b = q.y.c1; } break;
+        case P_MILLER: { if (t < 4) lds_st(sh.QA, t, t & 1 ? a : b); gtw_sync(); gtw_miller_loop(sh.G, sh.QA, a, b, sh.TB, sh.L, sh.S, t); } break;
+        case P_FP12MUL: if (t == 0) { fp12 x = gtw_to_reg(sh.F), y = gtw_to_reg(sh.G); gtw_from_reg(sh.G, fp12_mul(x, y)); } break;
         case P_LACC: if (t == 0) { lacc q; for (int i = 0; i < BLS_NL; i++) { q.pos[i] = a.l[i]; q.neg[i] = b.l[i]; } a = lacc_fin(q); } break;
       }
     }
