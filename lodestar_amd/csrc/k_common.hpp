@@ -240,3 +240,30 @@ __device__ jac<F> jac_mul_words(const jac<F>& P, const uint32_t* k, int nw) {
   return r;
 }
 
+
+// Small runs are latency-bound chains: a cooperative workgroup that shares its SIMDs with waves of the other branches'
+// kernels issues at a fraction of its rate (k_miller_coop: 1.7 ms alone in tools/microbench/lat_probe.hip, 3-4 ms in
+// a 128-set call's trace).  Launched with this much extra dynamic LDS, one such workgroup fills the CU's LDS (160 KB on
+// gfx950) beyond what any other kernel of the pipeline needs (<= 36 KB), so the CU runs it alone.  0 when the device
+// does not allow it (the launch then simply shares CUs).
+template <class Kernel>
+inline size_t exclusive_cu_lds(Kernel kernel) {
+  static const size_t pad = [&]() -> size_t {
+    int dev = 0, max_block = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&max_block, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&per_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess)
+      return 0;
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(kernel)) != hipSuccess) return 0;
+    // leave less than the smallest other kernel's LDS (14 KB) free on the CU
+    const size_t want = (size_t)per_cu - 8 * 1024;
+    if (per_cu <= 0 || (size_t)max_block < want || a.sharedSizeBytes >= want) return 0;
+    const size_t pad_b = want - a.sharedSizeBytes;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)pad_b) != hipSuccess)
+      return 0;
+    return pad_b;
+  }();
+  return pad;
+}

@@ -190,12 +190,16 @@ void launch_group_reduce(const PipelineBuffers& b, const uint32_t* f_ranges, uin
   if (ng) hipLaunchKernelGGL(k_group_reduce, dim3(ng), dim3(WAVE), 0, s, b, f_ranges, ng, F);
 }
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s,
-                        const uint32_t* sel, uint32_t n_sel, const uint32_t* G) {
+                        const uint32_t* sel, uint32_t n_sel, const uint32_t* G, bool exclusive) {
   const uint32_t n = sel ? n_sel : ng;
-  if (n) hipLaunchKernelGGL(k_group_check, dim3(n), dim3(GTW_LANES), 0, s, S, F, ng, G, sel, ok);
+  if (n)
+    hipLaunchKernelGGL(k_group_check, dim3(n), dim3(GTW_LANES), exclusive ? exclusive_cu_lds(k_group_check) : 0, s, S,
+                       F, ng, G, sel, ok);
 }
-void launch_group_sig_miller(const uint32_t* S, uint32_t ng, uint32_t* G, hipStream_t s) {
-  if (ng) hipLaunchKernelGGL(k_group_sig_miller, dim3(ng), dim3(GTW_LANES), 0, s, S, ng, G);
+void launch_group_sig_miller(const uint32_t* S, uint32_t ng, uint32_t* G, hipStream_t s, bool exclusive) {
+  if (ng)
+    hipLaunchKernelGGL(k_group_sig_miller, dim3(ng), dim3(GTW_LANES), exclusive ? exclusive_cu_lds(k_group_sig_miller) : 0,
+                       s, S, ng, G);
 }
 void launch_range_combine(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,
                           uint32_t n_out, uint32_t* S_out, uint32_t* F_out, hipStream_t s) {

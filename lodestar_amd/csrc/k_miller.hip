@@ -120,12 +120,14 @@ __global__ __launch_bounds__(GTW_LANES) void k_miller_coop(PipelineBuffers b) {
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
-void launch_miller_coop(const PipelineBuffers& b, bool units, hipStream_t s) {
+void launch_miller_coop(const PipelineBuffers& b, bool units, hipStream_t s, bool exclusive) {
   if (!b.n_chunks) return;
   if (units)
-    hipLaunchKernelGGL(k_miller_coop<true>, dim3(b.n_chunks), dim3(GTW_LANES), 0, s, b);
+    hipLaunchKernelGGL(k_miller_coop<true>, dim3(b.n_chunks), dim3(GTW_LANES),
+                       exclusive ? exclusive_cu_lds(k_miller_coop<true>) : 0, s, b);
   else
-    hipLaunchKernelGGL(k_miller_coop<false>, dim3(b.n_chunks), dim3(GTW_LANES), 0, s, b);
+    hipLaunchKernelGGL(k_miller_coop<false>, dim3(b.n_chunks), dim3(GTW_LANES),
+                       exclusive ? exclusive_cu_lds(k_miller_coop<false>) : 0, s, b);
 }
 
 void launch_miller_lines(const PipelineBuffers& b, hipStream_t s) {

@@ -113,7 +113,12 @@ void launch_miller_lines(const PipelineBuffers& b, hipStream_t s);
 void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s);
 // the same for chunks of ONE item each, as one cooperative 128-lane workgroup per pairing (lines on the fly; small
 // runs, for latency)
-void launch_miller_coop(const PipelineBuffers& b, bool units, hipStream_t s);
+// (exclusive: each workgroup takes a CU to itself -- k_common.hpp exclusive_cu_lds -- for latency-bound small runs;
+// BLSGPU_EXCLUSIVE_SMALL=0 turns it off everywhere)
+#ifndef BLSGPU_EXCLUSIVE_SMALL
+#define BLSGPU_EXCLUSIVE_SMALL 1
+#endif
+void launch_miller_coop(const PipelineBuffers& b, bool units, hipStream_t s, bool exclusive = false);
 // Batch groups: group g covers Miller chunks [f_ranges[2g], f_ranges[2g+1]).
 // reduce: F_g = prod f_chunk over chunks [f_ranges[2g], f_ranges[2g+1]) (W_FP12 SoA, stride n_groups); S_g comes
 // from launch_sig_msm (or, in the fallback, from per-set scalings summed by launch_group_reduce_lane)
@@ -123,8 +128,9 @@ void launch_group_reduce(const PipelineBuffers& b, const uint32_t* f_ranges, uin
 // (sel: check only the entries sel[0 .. n_sel), verdict q -> ok[q])
 // (G: MillerLoop(-g1, S_g) precomputed by launch_group_sig_miller, W_FP12 SoA stride n_groups; null = computed here)
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t n_groups, uint8_t* ok, hipStream_t s,
-                        const uint32_t* sel = nullptr, uint32_t n_sel = 0, const uint32_t* G = nullptr);
-void launch_group_sig_miller(const uint32_t* S, uint32_t n_groups, uint32_t* G, hipStream_t s);
+                        const uint32_t* sel = nullptr, uint32_t n_sel = 0, const uint32_t* G = nullptr,
+                        bool exclusive = false);
+void launch_group_sig_miller(const uint32_t* S, uint32_t n_groups, uint32_t* G, hipStream_t s, bool exclusive = false);
 // lane-per-item forms (one lane per range / sub-group) for the fallback's many tiny ranges
 void launch_group_reduce_lane(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
                               uint32_t n_groups, uint32_t* S, uint32_t* F, hipStream_t s);

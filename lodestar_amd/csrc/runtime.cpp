@@ -153,6 +153,7 @@ enum { kSig = 0, kMsg = 1, kPk = 2, kTail = 3, kStreams = 4 };
 #define BLSGPU_STREAM_PAIRS 1
 #endif
 
+
 struct Device {
   int id = 0;
   hipStream_t table_stream = nullptr;  // uploads and the synchronous helpers (debug, aggregate, ...)
@@ -715,7 +716,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     beg(5, sm);
     if (merged) launch_unit_aggregate(pb, sm);
     if (coop)
-      launch_miller_coop(pb, merged, sm);
+      launch_miller_coop(pb, merged, sm, BLSGPU_EXCLUSIVE_SMALL);
     else
       launch_miller_acc(pb, merged, sm);
     end(5, sm);
@@ -730,13 +731,13 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     end(4, s);
     // MillerLoop(-g1, S_g) of every group now, while the message branch still runs
     beg(kStages + 1, s);
-    launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, s);
+    launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, s, BLSGPU_EXCLUSIVE_SMALL && coop);
     end(kStages + 1, s);
     HIPCHK(hipEventRecord(sl.join_gsm, s));
     HIPCHK(hipStreamWaitEvent(stl, sl.join_gsm, 0));
     HIPCHK(hipStreamWaitEvent(stl, sl.join_msg, 0));
     beg(7, stl);
-    launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, stl, nullptr, 0, sl.d_G.p);
+    launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, stl, nullptr, 0, sl.d_G.p, BLSGPU_EXCLUSIVE_SMALL && coop);
     end(7, stl);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(sl.h_res.p, sl.d_res.p, o_ok + ng0, hipMemcpyDeviceToHost, stl));
