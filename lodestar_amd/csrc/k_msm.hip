@@ -5,13 +5,14 @@
 //                  LDS) give every lane a compact list of its signed set indices (LDS, no atomics, so the order
 //                  is deterministic); the lane then sums +-sig_i with mixed additions -> B[slice][t].  Lists keep
 //                  the wave's lanes busy on useful additions: ~len/8 per lane instead of len masked ones.
-//   k_msm_window   one lane per (range, window): W = sum_e (2e + 1) sum_{slices of the range} B_e
-//   k_msm_horner   two lanes per range: S_a and lambda S_b (8-window Horner passes, msm.hpp), then S = their sum,
-//                  written in the layout k_group_check reads
+//   k_msm_window   eight lanes per (range, window): W = sum_e (2e + 1) sum_{slices of the range} B_e
+//   k_msm_horner   two 16-lane groups per range: S_a and lambda S_b (8-window Horner passes, cooperative
+//                  doublings), then S = their sum, written in the layout k_group_check reads
 // Sets outside the batch equation (include == 0) and infinity signatures contribute nothing, as in the
 // per-set scaling this replaces.
 #include "k_common.hpp"
 #include "msm.hpp"
+#include "g2_coop.hpp"
 
 #define MSM_LANES (MSM_WINDOWS * MSM_BUCKETS)
 
@@ -57,36 +58,60 @@ __global__ __launch_bounds__(MSM_LANES) __attribute__((amdgpu_waves_per_eu(BLSGP
   st_g2j(B, n_slices * MSM_LANES, s * MSM_LANES + t, acc);
 }
 
-// range r covers slices [range_slices[r], range_slices[r + 1])
+// One lane per (range, window k, bucket e) -- the 8 lanes of a window are neighbours in one wave.  Range r covers
+// slices [range_slices[r], range_slices[r + 1]); the lane sums its bucket over them (4 slices of a 16k call: 3
+// additions), forms (2e + 1) B_e and the window's lanes sum their terms through LDS in a 3-level tree
+// (msm_odd_multiple / msm_window_sum_tree): W_k in 3 + 6 additions + 3 doublings of depth instead of 3 x 8 + 18.
 STAGE_KERNEL void k_msm_window(const uint32_t* range_slices, uint32_t n_ranges, const uint32_t* B, uint32_t n_slices,
                                uint32_t* W) {
-  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
-  if (q >= n_ranges * MSM_WINDOWS) return;
-  const uint32_t r = q / MSM_WINDOWS, k = q % MSM_WINDOWS;
-  const uint32_t s0 = range_slices[r], s1 = range_slices[r + 1];
-  const uint32_t nb = n_slices * MSM_LANES;
-  const g2j Wk = msm_window_sum([&](int e) {
-    g2j sum = jac_infinity<fp2>();
-    for (uint32_t s = s0; s < s1; s++) sum = jac_add(sum, ld_g2j(B, nb, s * MSM_LANES + k * MSM_BUCKETS + e));
-    return sum;
-  });
-  st_g2j(W, n_ranges * MSM_WINDOWS, q, Wk);
+  __shared__ uint32_t xch[W_G2J * WAVE];
+  const uint32_t t = threadIdx.x, q = blockIdx.x * WAVE + t;
+  const bool on = q < n_ranges * MSM_LANES;
+  const uint32_t r = q / MSM_LANES, tb = q % MSM_LANES, e = tb % MSM_BUCKETS;
+  g2j T = jac_infinity<fp2>();
+  if (on) {
+    const uint32_t s0 = range_slices[r], s1 = range_slices[r + 1], nb = n_slices * MSM_LANES;
+    if (s0 < s1) T = ld_g2j(B, nb, s0 * MSM_LANES + tb);
+#pragma unroll 1
+    for (uint32_t s = s0 + 1; s < s1; s++) T = jac_add(T, ld_g2j(B, nb, s * MSM_LANES + tb));
+    T = msm_odd_multiple(T, e);
+  }
+  static_assert(WAVE % MSM_BUCKETS == 0, "a window's lanes share a workgroup");
+#pragma unroll 1
+  for (uint32_t h = 1; h < MSM_BUCKETS; h <<= 1) {
+    if ((e & (2 * h - 1)) == h) st_g2j(xch, WAVE, t, T);
+    __syncthreads();
+    if ((e & (2 * h - 1)) == 0) T = jac_add(T, ld_g2j(xch, WAVE, t + h));
+    __syncthreads();
+  }
+  if (on && e == 0) st_g2j(W, n_ranges * MSM_WINDOWS, q / MSM_BUCKETS, T);
 }
 
-// lane pair (r, part) of one wave: part 1 leaves lambda S_b in its range's (already consumed) window-8 slot of W,
-// part 0 adds it after the barrier.  W is written and read within the workgroup, so no lane returns early.
-STAGE_KERNEL void k_msm_horner(uint32_t* W, uint32_t n_ranges, uint32_t* S) {
-  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
-  const uint32_t r = q >> 1, part = q & 1;
+// Horner passes on cooperative 16-lane groups (g2_coop.hpp): a workgroup of 128 lanes runs 4 ranges, group 2j the
+// S_a pass of range 4 blockIdx + j, group 2j + 1 its lambda S_b pass; the 28 doublings of a pass are cooperative
+// (3 product phases each), the 7 window additions and lambda run on the group's lane 0, then lane 0 of group 2j
+// adds its neighbour's lambda S_b from LDS.
+#define MSM_H_LANES 128
+#define MSM_H_RANGES (MSM_H_LANES / G2C_LANES / 2)
+__global__ __launch_bounds__(MSM_H_LANES) void k_msm_horner(const uint32_t* W, uint32_t n_ranges, uint32_t* S) {
+  __shared__ uint32_t lds[(MSM_H_LANES / G2C_LANES) * G2C_WORDS];
+  const uint32_t t = threadIdx.x, grp = t / G2C_LANES, tg = t % G2C_LANES;
+  const uint32_t r = blockIdx.x * MSM_H_RANGES + grp / 2, part = grp & 1;
   const bool on = r < n_ranges;
-  const uint32_t nw = n_ranges * MSM_WINDOWS;
-  g2j H;
-  if (on) {
-    H = msm_horner_half([&](int k) { return ld_g2j(W, nw, r * MSM_WINDOWS + k); }, (int)part);
-    if (part) st_g2j(W, nw, r * MSM_WINDOWS + MSM_WINDOWS / 2, H);
+  const uint32_t nw = n_ranges * MSM_WINDOWS, base = r * MSM_WINDOWS + part * (MSM_WINDOWS / 2);
+  uint32_t* g = lds + grp * G2C_WORDS;
+  if (tg == 0) g2c_st_point(g, on ? ld_g2j(W, nw, base + MSM_WINDOWS / 2 - 1) : jac_infinity<fp2>());
+  g2c_sync();
+#pragma unroll 1
+  for (int k = MSM_WINDOWS / 2 - 2; k >= 0; k--) {
+#pragma unroll 1
+    for (int d = 0; d < 4; d++) g2c_dbl(g, tg);
+    if (tg == 0 && on) g2c_st_point(g, jac_add(g2c_ld_point(g), ld_g2j(W, nw, base + (uint32_t)k)));
+    g2c_sync();
   }
-  __syncthreads();
-  if (on && !part) st_g2j(S, n_ranges, r, jac_add(H, ld_g2j(W, nw, r * MSM_WINDOWS + MSM_WINDOWS / 2)));
+  if (tg == 0 && on && part) g2c_st_point(g, endo_lambda(g2c_ld_point(g)));
+  g2c_sync();
+  if (tg == 0 && on && !part) st_g2j(S, n_ranges, r, jac_add(g2c_ld_point(g), g2c_ld_point(g + G2C_WORDS)));
 }
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
@@ -94,8 +119,11 @@ static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 void launch_sig_msm(const PipelineBuffers& b, const uint32_t* slices, uint32_t n_slices, const uint32_t* range_slices,
                     uint32_t n_ranges, uint32_t* B, uint32_t* W, uint32_t* S, hipStream_t st) {
   if (!n_ranges) return;
-  if (n_slices) hipLaunchKernelGGL(k_msm_bucket, dim3(n_slices), dim3(MSM_LANES), 0, st, b, slices, n_slices, B);
-  hipLaunchKernelGGL(k_msm_window, grid_for(n_ranges * MSM_WINDOWS), dim3(WAVE), 0, st, range_slices, n_ranges, B,
+  if (n_slices) {
+    hipLaunchKernelGGL(k_msm_bucket, dim3(n_slices), dim3(MSM_LANES), 0, st, b, slices, n_slices, B);
+  }
+  hipLaunchKernelGGL(k_msm_window, grid_for(n_ranges * MSM_LANES), dim3(WAVE), 0, st, range_slices, n_ranges, B,
                      n_slices, W);
-  hipLaunchKernelGGL(k_msm_horner, grid_for(2 * n_ranges), dim3(WAVE), 0, st, W, n_ranges, S);
+  hipLaunchKernelGGL(k_msm_horner, dim3((n_ranges + MSM_H_RANGES - 1) / MSM_H_RANGES), dim3(MSM_H_LANES), 0, st, W,
+                     n_ranges, S);
 }

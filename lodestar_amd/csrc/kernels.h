@@ -97,7 +97,9 @@ void launch_sig_scale(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s, 
 // S_r = sum r_i sig_i over the included sets of each range, as a bucket MSM (k_msm.hip, msm.hpp).  Range r is the
 // slices [range_slices[r], range_slices[r+1]); slice s is the sets [slices[2s], slices[2s+1]) (<= MSM_SLICE of
 // them).  B: MSM_BUCKET_WORDS words per slice, W: MSM_WINDOW_WORDS per range; S: W_G2J SoA, stride n_ranges.
+#ifndef MSM_SLICE
 #define MSM_SLICE 256
+#endif
 #define MSM_BUCKET_WORDS (128 * W_G2J)
 #define MSM_WINDOW_WORDS (16 * W_G2J)
 void launch_sig_msm(const PipelineBuffers& b, const uint32_t* slices, uint32_t n_slices, const uint32_t* range_slices,

@@ -96,7 +96,7 @@ static g2j emu_msm_core(const g2a* P, const uint64_t* w, const uint8_t* active, 
     }
   }
   static g2j W[MSM_WINDOWS];
-  for (int k = 0; k < MSM_WINDOWS; k++) W[k] = msm_window_sum([&](int e) { return B[k][e]; });
+  for (int k = 0; k < MSM_WINDOWS; k++) W[k] = msm_window_sum_tree([&](int e) { return B[k][e]; });
   return msm_horner([&](int k) { return W[k]; });
 }
 extern "C" {
