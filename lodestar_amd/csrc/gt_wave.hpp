@@ -382,7 +382,7 @@ __device__ void gtw_add_step(uint32_t* TB, const uint32_t* QA, uint32_t* L, cons
   gtw_sync();
 }
 
-__device__ void gtw_miller_loop(uint32_t* F, const uint32_t* QA, const fp& xP, const fp& yP, uint32_t* TB, uint32_t* L,
+__device__ __forceinline__ void gtw_miller_loop(uint32_t* F, const uint32_t* QA, const fp& xP, const fp& yP, uint32_t* TB, uint32_t* L,
                                 uint32_t* S, uint32_t t) {
   if (t < 6) lds_st(TB, t, t < 4 ? lds_ld(QA, t) : (t == 4 ? FP_ONE : fp_zero()));
   gtw_set_one(F, t);  // (syncs)
