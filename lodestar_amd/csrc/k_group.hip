@@ -50,6 +50,42 @@ __global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const 
   if (lane == 0) st_fp12(F_out, ng, g, F);
 }
 
+// ---- F_g as a product tree (the batch pass) ---------------------------------------------------------------
+// k_group_reduce above multiplies a group's chunks one wave per group: ~log2(chunks) + chunks / 64 lane-serial Fp12
+// products deep (2.25 ms of a 16k call's critical path, 0.8 ms of a 128-set call's).  The tree form:
+//   k_f_runs    lane per run of K consecutive chunks of a group (large runs only): their product into the run's first
+//   k_f_pairs   one 128-lane workgroup per pair (dst, src) of one tree level: f[dst] *= f[src] as a cooperative
+//               Fp12 product (gt_wave.hpp gtw_mul, ~5 us); the host plans the levels (runtime.cpp plan_f_tree)
+//   k_f_gather  lane per (group, word): F_g = the group's first chunk (one for a group without chunks)
+STAGE_KERNEL void k_f_runs(PipelineBuffers b, const uint32_t* runs, uint32_t n_runs) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  if (q >= n_runs) return;
+  const uint32_t a = runs[2 * q], e = runs[2 * q + 1];
+  fp12 F = ld_fp12(b.f_chunk, b.n, a);
+#pragma unroll 1
+  for (uint32_t i = a + 1; i < e; i++) F = fp12_mul(F, ld_fp12(b.f_chunk, b.n, i));
+  st_fp12(b.f_chunk, b.n, a, F);
+}
+
+__global__ __launch_bounds__(GTW_LANES) void k_f_pairs(PipelineBuffers b, const uint32_t* pairs) {
+  __shared__ uint32_t A[GTW_FP12], B[GTW_FP12], S[108 * BLS_NL];
+  const uint32_t t = threadIdx.x, i = pairs[2 * blockIdx.x], j = pairs[2 * blockIdx.x + 1];
+  for (uint32_t w = t; w < W_FP12; w += GTW_LANES) {
+    A[gtw_lds_word(w)] = b.f_chunk[(size_t)w * b.n + i];
+    B[gtw_lds_word(w)] = b.f_chunk[(size_t)w * b.n + j];
+  }
+  gtw_sync();
+  gtw_mul<false>(A, A, B, S, t);
+  for (uint32_t w = t; w < W_FP12; w += GTW_LANES) b.f_chunk[(size_t)w * b.n + i] = A[gtw_lds_word(w)];
+}
+
+STAGE_KERNEL void k_f_gather(PipelineBuffers b, const uint32_t* f_ranges, uint32_t ng, uint32_t* F_out) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  if (q >= ng * W_FP12) return;
+  const uint32_t g = q % ng, w = q / ng, a = f_ranges[2 * g], e = f_ranges[2 * g + 1];
+  F_out[q] = a < e ? b.f_chunk[(size_t)w * b.n + a] : (w < BLS_NL ? FP_ONE.l[w] : 0u);
+}
+
 // One 128-lane workgroup per group: the Miller loop and the final exponentiation run as cooperative Fp12
 // arithmetic (gt_wave.hpp), one Fp product per lane per step.
 //   G_in == nullptr: FinalExp(F * MillerLoop(-g1, S)) == 1 (the fallback's per-job / sub-group checks);
@@ -188,6 +224,18 @@ void launch_job_mask(const PipelineBuffers& b, hipStream_t s) {
 }
 void launch_group_reduce(const PipelineBuffers& b, const uint32_t* f_ranges, uint32_t ng, uint32_t* F, hipStream_t s) {
   if (ng) hipLaunchKernelGGL(k_group_reduce, dim3(ng), dim3(WAVE), 0, s, b, f_ranges, ng, F);
+}
+void launch_group_tree(const PipelineBuffers& b, const uint32_t* f_ranges, uint32_t ng, const uint32_t* runs,
+                       uint32_t n_runs, const uint32_t* pairs, const std::vector<uint32_t>& level_end, uint32_t* F,
+                       hipStream_t s) {
+  if (!ng) return;
+  if (n_runs) hipLaunchKernelGGL(k_f_runs, grid_for(n_runs), dim3(WAVE), 0, s, b, runs, n_runs);
+  uint32_t p0 = 0;
+  for (const uint32_t p1 : level_end) {
+    if (p1 > p0) hipLaunchKernelGGL(k_f_pairs, dim3(p1 - p0), dim3(GTW_LANES), 0, s, b, pairs + 2 * (size_t)p0);
+    p0 = p1;
+  }
+  hipLaunchKernelGGL(k_f_gather, grid_for(ng * W_FP12), dim3(WAVE), 0, s, b, f_ranges, ng, F);
 }
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s,
                         const uint32_t* sel, uint32_t n_sel, const uint32_t* G, bool exclusive) {

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <vector>
 
 // Word counts of the SoA records (element i, word w at base[w * stride + i])
 #define W_FP 14
@@ -126,6 +127,12 @@ void launch_miller_coop(const PipelineBuffers& b, bool units, hipStream_t s, boo
 // from launch_sig_msm (or, in the fallback, from per-set scalings summed by launch_group_reduce_lane)
 void launch_group_reduce(const PipelineBuffers& b, const uint32_t* f_ranges, uint32_t n_groups, uint32_t* F,
                          hipStream_t s);
+// the same F_g as a product tree (k_group.hip): runs[0 .. n_runs) (first, end) chunk runs multiplied lane-serially
+// into their first chunk, then the pair levels (pairs up to level_end[0], then up to level_end[1], ...: f[dst] *=
+// f[src], one cooperative workgroup per pair), then F_g = f[first chunk of g]
+void launch_group_tree(const PipelineBuffers& b, const uint32_t* f_ranges, uint32_t n_groups, const uint32_t* runs,
+                       uint32_t n_runs, const uint32_t* pairs, const std::vector<uint32_t>& level_end, uint32_t* F,
+                       hipStream_t s);
 // check: ok_g = FinalExp(F_g * MillerLoop(-g1, S_g)) == 1
 // (sel: check only the entries sel[0 .. n_sel), verdict q -> ok[q])
 // (G: MillerLoop(-g1, S_g) precomputed by launch_group_sig_miller, W_FP12 SoA stride n_groups; null = computed here)

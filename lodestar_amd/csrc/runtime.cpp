@@ -518,6 +518,29 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     add_slices(slices, range_slices, job_sets(group_jobs[g].first).first, job_sets(group_jobs[g].second - 1).second,
                slice_len);
   const uint32_t n_slices = (uint32_t)(slices.size() / 2);
+  // F_g = prod of the group's Miller chunks as a product tree (launch_group_tree): with more than 8192 chunks, runs
+  // of f_k consecutive chunks first (lane-serial: a 128-lane cooperative product costs ~6x the lane time), then
+  // pair levels of stride f_k, 2 f_k, ... (one cooperative workgroup per pair); ftree = runs, then the pairs
+  std::vector<uint32_t> ftree, f_level_end;
+  uint32_t f_k = 1, f_max = 0;
+  while (n_chunks / f_k > 8192 && f_k < 16) f_k *= 2;
+  for (uint32_t g = 0; g < ng0; g++) f_max = std::max(f_max, g_chunks[2 * g + 1] - g_chunks[2 * g]);
+  if (f_k > 1)
+    for (uint32_t g = 0; g < ng0; g++)
+      for (uint32_t x = g_chunks[2 * g], e = g_chunks[2 * g + 1]; x < e; x += f_k)
+        if (std::min(e, x + f_k) - x > 1) {
+          ftree.push_back(x);
+          ftree.push_back(std::min(e, x + f_k));
+        }
+  const uint32_t n_fruns = (uint32_t)(ftree.size() / 2);
+  for (uint32_t st = f_k; st < f_max; st *= 2) {
+    for (uint32_t g = 0; g < ng0; g++)
+      for (uint32_t i = g_chunks[2 * g], e = g_chunks[2 * g + 1]; i + st < e; i += 2 * st) {
+        ftree.push_back(i);
+        ftree.push_back(i + st);
+      }
+    f_level_end.push_back((uint32_t)(ftree.size() / 2) - n_fruns);
+  }
   // sets that aggregate >= 2 keys (one wave each in k_pk_aggregate); one-key sets are read by k_pk_finish
   std::vector<uint32_t> agg_sets;
   if (table_mode || bytes_agg)
@@ -526,7 +549,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
 
   // ---- stage inputs in the pinned arena and copy it to the device in one transfer ------------------------
   // arena (256-B aligned sections): scalars | job_first_set | sigs (192 B each) | sig_len | unique msgs |
-  // msg_idx | set ranges | f ranges | units (first, sets, msg) | pk section
+  // msg_idx | set ranges | f ranges | units (first, sets, msg) | chunks | agg sets | MSM slices | F tree | pk section
   const size_t o_scal = 0, o_jobs = al256(o_scal + (size_t)n * 8), o_sigs = al256(o_jobs + (size_t)(nj + 1) * 4),
                o_siglen = al256(o_sigs + (size_t)n * 192), o_umsg = al256(o_siglen + (size_t)n * 4),
                o_midx = al256(o_umsg + (size_t)n_umsg * 32), o_ranges = al256(o_midx + (size_t)n * 4),
@@ -535,7 +558,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
                o_usets = al256(o_ufirst + (size_t)(n_units + 1) * 4), o_umsgi = al256(o_usets + (size_t)unit_sets.size() * 4),
                o_cfirst = al256(o_umsgi + (size_t)n_units * 4), o_citems = al256(o_cfirst + (size_t)(n_chunks + 1) * 4),
                o_agg = al256(o_citems + chunk_items.size() * 4), o_slices = al256(o_agg + agg_sets.size() * 4),
-               o_rslices = al256(o_slices + slices.size() * 4), o_pk = al256(o_rslices + range_slices.size() * 4);
+               o_rslices = al256(o_slices + slices.size() * 4), o_ftree = al256(o_rslices + range_slices.size() * 4),
+               o_pk = al256(o_ftree + ftree.size() * 4);
   size_t in_bytes;
   if (table_mode)
     in_bytes = al256(o_pk + (size_t)(n + 1) * 4) + (size_t)npk * 4;
@@ -577,6 +601,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   if (!agg_sets.empty()) memcpy(hin + o_agg, agg_sets.data(), agg_sets.size() * 4);
   if (!slices.empty()) memcpy(hin + o_slices, slices.data(), slices.size() * 4);
   memcpy(hin + o_rslices, range_slices.data(), range_slices.size() * 4);
+  if (!ftree.empty()) memcpy(hin + o_ftree, ftree.data(), ftree.size() * 4);
   if (merged) {
     memcpy(hin + o_ufirst, unit_first.data(), (size_t)(n_units + 1) * 4);
     memcpy(hin + o_usets, unit_sets.data(), unit_sets.size() * 4);
@@ -728,7 +753,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     end(5, sm);
     const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
     beg(6, sm);
-    launch_group_reduce(pb, d_franges, ng0, sl.d_F.p, sm);
+    const uint32_t* d_ftree = reinterpret_cast<uint32_t*>(din + o_ftree);
+    launch_group_tree(pb, d_franges, ng0, d_ftree, n_fruns, d_ftree + 2 * (size_t)n_fruns, f_level_end, sl.d_F.p, sm);
     end(6, sm);
     HIPCHK(hipEventRecord(sl.join_msg, sm));
     const uint32_t* d_slices = reinterpret_cast<uint32_t*>(din + o_slices);

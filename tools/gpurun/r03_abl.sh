@@ -1,0 +1,13 @@
+# usage: bash tools/gpurun/r03_abl.sh TAG ROUNDS LIB... -- GPU tests (default library), interleaved 100-step C2
+# lines of the libraries, then serial kernel traces (C1, C2; one call in flight) of the default library
+set -e
+TAG=$1; R=$2; shift 2
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
+for i in $(seq 1 $R); do
+  for L in "$@"; do
+    BLSGPU_LIB=$GRAFT_REPO_ROOT/lodestar_amd/$L timeout -k 10 200 python bench.py --no-cpu-baseline --no-parity --steps 100 --warmup 5 > gpurun_out/${TAG}_${L%.so}_$i.json 2> gpurun_out/${TAG}_${L%.so}_$i.err
+  done
+done
+bash tools/gpurun/r03_lat.sh $TAG C1 C2
