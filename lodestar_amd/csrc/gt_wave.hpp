@@ -21,13 +21,15 @@
 #define GTW_LANES 128
 #define GTW_FP12 (12 * BLS_NL)
 
+#if defined(__HIPCC__)
 BLS_INL void gtw_sync() { __syncthreads(); }
+#endif
 
 // ---------------------------------------------------------------------------------------------------
 // C = A * B (C may alias A or B).  SPARSE: B is a Miller line with w-coefficients 0, 2, 3 only.
 // ---------------------------------------------------------------------------------------------------
 template <bool SPARSE>
-__device__ void gtw_mul(uint32_t* C, const uint32_t* A, const uint32_t* B, uint32_t* S, uint32_t t) {
+BLS_INL void gtw_mul_prod(const uint32_t* A, const uint32_t* B, uint32_t* S, uint32_t t) {
   constexpr uint32_t NP = SPARSE ? 54 : 108;
   if (t < NP) {
     const int pr = t / 3, c = t % 3;
@@ -44,7 +46,9 @@ __device__ void gtw_mul(uint32_t* C, const uint32_t* A, const uint32_t* B, uint3
     kara_operands(lds_ld(A, 2 * i), lds_ld(A, 2 * i + 1), lds_ld(B, 2 * j), lds_ld(B, 2 * j + 1), c, X, Y);
     lds_st(S, t, fp_mul(X, Y));
   }
-  gtw_sync();
+}
+template <bool SPARSE>
+BLS_INL void gtw_mul_rec(uint32_t* C, const uint32_t* S, uint32_t t) {
   if (t < 12) {
     const int k = t >> 1, comp = t & 1;
     lacc acc;
@@ -81,6 +85,14 @@ __device__ void gtw_mul(uint32_t* C, const uint32_t* A, const uint32_t* B, uint3
     }
     lds_st(C, t, lacc_fin(acc));
   }
+}
+#if defined(__HIPCC__)
+// the two phases in sequence
+template <bool SPARSE>
+__device__ void gtw_mul(uint32_t* C, const uint32_t* A, const uint32_t* B, uint32_t* S, uint32_t t) {
+  gtw_mul_prod<SPARSE>(A, B, S, t);
+  gtw_sync();
+  gtw_mul_rec<SPARSE>(C, S, t);
   gtw_sync();
 }
 
@@ -271,13 +283,25 @@ __device__ void gtw_final_exp(uint32_t* F, uint32_t* W, uint32_t* S, uint32_t t)
   gtw_mul<false>(F, T, U, S, t);  // t m^3
 }
 
+#endif  // __HIPCC__
+
 // ---------------------------------------------------------------------------------------------------
 // Miller loop f = conj(f_{|z|,Q}(P)) into F (as pairing.hpp miller_loop).  Q affine in LDS (QA: 4 Fp:
 // x.re, x.im, y.re, y.im), P = (xP, yP) uniform.  TB: T (6 Fp), then the doubling-step temporaries
-// (16 Fp).  L: an Fp12-layout line buffer (w-coefficients 0, 2, 3 used).
+// (14 Fp).  L0 / L1: Fp12-layout line buffers (w-coefficients 0, 2, 3 used), S2: the T chain's products.
+//
+// Three waves (GTW_MILLER_LANES): waves 1-2 update f (square: 108 products + recombination; times the sparse
+// line: 54 + recombination -- four barrier-separated phases per step) while wave 0 computes the NEXT step's line
+// from T in the same four phases (doubling: products, linear combination, products, linear combination; addition:
+// lane-serial in the first phase, on lane 0: its Fp2 products use fp2_mul's per-lane LDS slot, tower.hpp, which
+// covers lanes 0 .. 127 only -- the f lanes use none).  The line chain depends only on T, so it leaves the critical path of the f
+// chain; the line of step s sits in L[s & 1].  Divergent lanes of ONE wave would run both paths in turn, hence a
+// wave of its own.
 // ---------------------------------------------------------------------------------------------------
-__device__ void gtw_dbl_step(uint32_t* TB, uint32_t* L, const fp& xP, const fp& yP, uint32_t* S, uint32_t t) {
-  uint32_t* D = TB + 6 * BLS_NL;
+#define GTW_MILLER_LANES (GTW_LANES + 64)
+
+// doubling step phases (lane t of the T-chain wave, products in S)
+BLS_INL void gtw_dbl_p1(const uint32_t* TB, uint32_t* S, uint32_t t) {
   // phase 1: x y (Karatsuba, 3), y^2 (2), z^2 (2), (y + z)^2 (2), x^2 (2)
   if (t < 11) {
     const fp x0 = lds_ld(TB, 0), x1 = lds_ld(TB, 1), y0 = lds_ld(TB, 2), y1 = lds_ld(TB, 3);
@@ -296,7 +320,9 @@ __device__ void gtw_dbl_step(uint32_t* TB, uint32_t* L, const fp& xP, const fp& 
     }
     lds_st(S, t, fp_mul(X, Y));
   }
-  gtw_sync();
+}
+BLS_INL void gtw_dbl_p2(uint32_t* TB, uint32_t* L, const uint32_t* S, uint32_t t) {
+  uint32_t* D = TB + 6 * BLS_NL;
   // phase 2 (component lanes): A = xy/2, E = 12 xi C, F = 3E, G = (B + F)/2, H = (y+z)^2 - B - C, 3J,
   // B - F, l0 = E - B.  D slots (Fp2): 0 A, 1 B-F, 2 G, 3 E, 4 B, 5 H, 6 3J
   if (t < 2) {
@@ -319,7 +345,9 @@ __device__ void gtw_dbl_step(uint32_t* TB, uint32_t* L, const fp& xP, const fp& 
     lds_st(D, 12 + c, fp_mul3(lds_ld(S, 9 + c)));
     lds_st(L, 0 + c, fp_sub(E, B));  // l0 at w^0
   }
-  gtw_sync();
+}
+BLS_INL void gtw_dbl_p3(const uint32_t* TB, uint32_t* S, const fp& xP, const fp& yP, uint32_t t) {
+  const uint32_t* D = TB + 6 * BLS_NL;
   // phase 3: A (B - F) (3), G^2 (2), E^2 (2), B H (3), 3J xP (2), H yP (2)
   if (t < 14) {
     fp X, Y;
@@ -340,7 +368,8 @@ __device__ void gtw_dbl_step(uint32_t* TB, uint32_t* L, const fp& xP, const fp& 
     }
     lds_st(S, t, fp_mul(X, Y));
   }
-  gtw_sync();
+}
+BLS_INL void gtw_dbl_p4(uint32_t* TB, uint32_t* L, const uint32_t* S, uint32_t t) {
   // phase 4: T = (A(B-F), G^2 - 3E^2, B H), l1 = 3J xP at w^2, l4 = -H yP at w^3
   if (t < 2) {
     const int c = t;
@@ -352,10 +381,10 @@ __device__ void gtw_dbl_step(uint32_t* TB, uint32_t* L, const fp& xP, const fp& 
     lds_st(L, 4 + c, lds_ld(S, 10 + c));
     lds_st(L, 6 + c, fp_neg(lds_ld(S, 12 + c)));
   }
-  gtw_sync();
 }
 
-__device__ void gtw_add_step(uint32_t* TB, const uint32_t* QA, uint32_t* L, const fp& xP, const fp& yP, uint32_t t) {
+BLS_INL void gtw_add_step_lane(uint32_t* TB, const uint32_t* QA, uint32_t* L, const fp& xP, const fp& yP,
+                               uint32_t t) {
   if (t == 0) {
     g2proj T;
     T.x = fp2_make(lds_ld(TB, 0), lds_ld(TB, 1));
@@ -379,29 +408,95 @@ __device__ void gtw_add_step(uint32_t* TB, const uint32_t* QA, uint32_t* L, cons
     lds_st(L, 6, l4.c0);
     lds_st(L, 7, l4.c1);
   }
-  gtw_sync();
 }
 
-__device__ __forceinline__ void gtw_miller_loop(uint32_t* F, const uint32_t* QA, const fp& xP, const fp& yP, uint32_t* TB, uint32_t* L,
-                                uint32_t* S, uint32_t t) {
-  if (t < 6) lds_st(TB, t, t < 4 ? lds_ld(QA, t) : (t == 4 ? FP_ONE : fp_zero()));
-  gtw_set_one(F, t);  // (syncs)
-  int bit = 62;
-  bool add_next = false;
+// The loop as a schedule of phases: run(f) executes phase f for every lane of the workgroup (on the device: the
+// calling lane, then a barrier; in the host model, tests/native/emu.cpp: lanes 0 .. GTW_MILLER_LANES - 1 in turn --
+// within a phase no lane reads what another writes).
+template <class Run>
+BLS_INL void gtw_miller_schedule(Run&& run, uint32_t* F, const uint32_t* QA, const fp& xP, const fp& yP, uint32_t* TB,
+                                 uint32_t* L0, uint32_t* L1, uint32_t* S, uint32_t* S2) {
+  constexpr uint32_t TW = 64;  // lanes < TW: the T-chain wave; lane TW + i: f-lane i
+  run([&](uint32_t t) {
+    if (t < 6) lds_st(TB, (int)t, t < 4 ? lds_ld(QA, (int)t) : (t == 4 ? FP_ONE : fp_zero()));
+    if (t < 12) lds_st(F, (int)t, t == 0 ? FP_ONE : fp_zero());
+  });
+  // the line of step 0 (a doubling)
+  run([&](uint32_t t) {
+    if (t < TW) gtw_dbl_p1(TB, S2, t);
+  });
+  run([&](uint32_t t) {
+    if (t < TW) gtw_dbl_p2(TB, L0, S2, t);
+  });
+  run([&](uint32_t t) {
+    if (t < TW) gtw_dbl_p3(TB, S2, xP, yP, t);
+  });
+  run([&](uint32_t t) {
+    if (t < TW) gtw_dbl_p4(TB, L0, S2, t);
+  });
+  int bit = 61;
+  bool add_next = (BLS_Z_ABS >> 62) & 1ull, cur_add = false;
 #pragma unroll 1
   for (int s = 0; s < 68; s++) {
-    if (!add_next) {
-      if (s != 0) gtw_mul<false>(F, F, F, S, t);
-      gtw_dbl_step(TB, L, xP, yP, S, t);
-      add_next = (BLS_Z_ABS >> bit) & 1ull;
-      bit--;
-    } else {
-      gtw_add_step(TB, QA, L, xP, yP, t);
-      add_next = false;
+    uint32_t* cur = (s & 1) ? L1 : L0;
+    uint32_t* nxt = (s & 1) ? L0 : L1;
+    const bool more = s + 1 < 68, next_add = add_next;
+    if (more) {
+      if (next_add) {
+        add_next = false;
+      } else {
+        add_next = (BLS_Z_ABS >> bit) & 1ull;
+        bit--;
+      }
     }
-    gtw_mul<true>(F, F, L, S, t);
+    const bool sq = !cur_add && s != 0;
+    const bool dbl = more && !next_add;
+    run([&](uint32_t t) {
+      if (t >= TW) {
+        if (sq) gtw_mul_prod<false>(F, F, S, t - TW);
+      } else if (more) {
+        if (next_add)
+          gtw_add_step_lane(TB, QA, nxt, xP, yP, t);
+        else
+          gtw_dbl_p1(TB, S2, t);
+      }
+    });
+    run([&](uint32_t t) {
+      if (t >= TW) {
+        if (sq) gtw_mul_rec<false>(F, S, t - TW);
+      } else if (dbl) {
+        gtw_dbl_p2(TB, nxt, S2, t);
+      }
+    });
+    run([&](uint32_t t) {
+      if (t >= TW)
+        gtw_mul_prod<true>(F, cur, S, t - TW);
+      else if (dbl)
+        gtw_dbl_p3(TB, S2, xP, yP, t);
+    });
+    run([&](uint32_t t) {
+      if (t >= TW)
+        gtw_mul_rec<true>(F, S, t - TW);
+      else if (dbl)
+        gtw_dbl_p4(TB, nxt, S2, t);
+    });
+    cur_add = next_add;
   }
-  gtw_conj(F, F, t);
+  run([&](uint32_t t) {  // f = conj(f): negate the odd w-coefficients
+    if (t < 12 && ((t >> 1) & 1)) lds_st(F, (int)t, fp_neg(lds_ld(F, (int)t)));
+  });
+}
+
+#if defined(__HIPCC__)
+__device__ __forceinline__ void gtw_miller_loop(uint32_t* F, const uint32_t* QA, const fp& xP, const fp& yP,
+                                                uint32_t* TB, uint32_t* L0, uint32_t* L1, uint32_t* S, uint32_t* S2,
+                                                uint32_t t) {
+  gtw_miller_schedule(
+      [&](auto&& phase) {
+        phase(t);
+        gtw_sync();
+      },
+      F, QA, xP, yP, TB, L0, L1, S, S2);
 }
 
 // Fp12 word w of the SoA tower layout in HBM (Fp2 slots c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2, W_FP words per
@@ -411,6 +506,7 @@ __device__ __forceinline__ uint32_t gtw_lds_word(uint32_t w) {
   const uint32_t k = slot < 3 ? 2 * slot : 2 * (slot - 3) + 1;
   return k * 2 * BLS_NL + rest;
 }
+#endif  // __HIPCC__
 
 // LDS footprint of one cooperative group check (words)
 struct GtwLds {
@@ -418,7 +514,9 @@ struct GtwLds {
   uint32_t F[GTW_FP12];         // accumulator
   uint32_t G[GTW_FP12];         // Miller value
   uint32_t W[5 * GTW_FP12];     // final-exponentiation temporaries
-  uint32_t L[GTW_FP12];         // line
+  uint32_t L[GTW_FP12];         // lines (two buffers)
+  uint32_t L1[GTW_FP12];
+  uint32_t S2[14 * BLS_NL];     // the Miller loop's T-chain products
   uint32_t TB[(6 + 14) * BLS_NL];  // T + doubling temporaries
   uint32_t QA[4 * BLS_NL];      // Q affine
   uint32_t flag;

@@ -246,8 +246,10 @@ __device__ jac<F> jac_mul_words(const jac<F>& P, const uint32_t* k, int nw) {
 // a 128-set call's trace).  Launched with this much extra dynamic LDS, one such workgroup fills the CU's LDS (160 KB on
 // gfx950) beyond what any other kernel of the pipeline needs (<= 36 KB), so the CU runs it alone.  0 when the device
 // does not allow it (the launch then simply shares CUs).
-template <class Kernel>
-inline size_t exclusive_cu_lds(Kernel kernel) {
+// (One cached value per kernel: the template parameter is the kernel itself -- keyed by its type, kernels of one
+// signature shared the first one's padding, and a larger kernel's static LDS plus that padding overflowed the CU.)
+template <auto kernel>
+inline size_t exclusive_cu_lds() {
   static const size_t pad = [&]() -> size_t {
     int dev = 0, max_block = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;

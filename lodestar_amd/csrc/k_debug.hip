@@ -138,7 +138,7 @@ __global__ __launch_bounds__(WAVE) void k_debug_op(int op, uint32_t n, const uin
 // Workgroup-cooperative GT engine (gt_wave.hpp), one element per 128-lane block:
 //   op 16: final exponentiation of an Fp12 (576 B) -> Fp12
 //   op 17: Miller loop of (P: G1 affine 96 B, Q: G2 affine 192 B) -> Fp12
-__global__ __launch_bounds__(GTW_LANES) void k_debug_gt(int op, const uint8_t* in, uint32_t in_stride, uint8_t* out,
+__global__ __launch_bounds__(GTW_MILLER_LANES) void k_debug_gt(int op, const uint8_t* in, uint32_t in_stride, uint8_t* out,
                                                          uint32_t out_stride, int32_t* status) {
   __shared__ GtwLds sh;
   const uint32_t i = blockIdx.x, t = threadIdx.x;
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(GTW_LANES) void k_debug_gt(int op, const uint8_t* i
     gtw_sync();
     const fp xP = lds_ld(sh.L, 0), yP = lds_ld(sh.L, 1);
     gtw_sync();
-    gtw_miller_loop(sh.F, sh.QA, xP, yP, sh.TB, sh.L, sh.S, t);
+    gtw_miller_loop(sh.F, sh.QA, xP, yP, sh.TB, sh.L, sh.L1, sh.S, sh.S2, t);
   }
   if (t == 0) {
     dbg_store_fp12(gtw_to_reg(sh.F), o);
@@ -176,7 +176,7 @@ void launch_debug_op(int op, uint32_t n, const uint8_t* in, uint32_t in_stride, 
                      int32_t* status, hipStream_t s) {
   if (!n) return;
   if (op == 16 || op == 17)
-    hipLaunchKernelGGL(k_debug_gt, dim3(n), dim3(GTW_LANES), 0, s, op, in, in_stride, out, out_stride, status);
+    hipLaunchKernelGGL(k_debug_gt, dim3(n), dim3(GTW_MILLER_LANES), 0, s, op, in, in_stride, out, out_stride, status);
   else
     hipLaunchKernelGGL(k_debug_op, grid_for(n), dim3(WAVE), 0, s, op, n, in, in_stride, out, out_stride, status);
 }

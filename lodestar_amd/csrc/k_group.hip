@@ -107,25 +107,25 @@ __device__ __forceinline__ void gtw_load_S(GtwLds& sh, const uint32_t* S_in, uin
   }
 }
 
-__global__ __launch_bounds__(GTW_LANES) void k_group_sig_miller(const uint32_t* S_in, uint32_t ng, uint32_t* G_out) {
+__global__ __launch_bounds__(GTW_MILLER_LANES) void k_group_sig_miller(const uint32_t* S_in, uint32_t ng, uint32_t* G_out) {
   __shared__ GtwLds sh;
   const uint32_t g = blockIdx.x, t = threadIdx.x;
   gtw_load_S(sh, S_in, ng, g, t);
   gtw_sync();
   if (sh.flag)
-    gtw_miller_loop(sh.G, sh.QA, G1_GEN_X, G1_NEG_GEN_Y, sh.TB, sh.L, sh.S, t);
+    gtw_miller_loop(sh.G, sh.QA, G1_GEN_X, G1_NEG_GEN_Y, sh.TB, sh.L, sh.L1, sh.S, sh.S2, t);
   else
     gtw_set_one(sh.G, t);
   gtw_sync();
-  for (uint32_t w = t; w < W_FP12; w += GTW_LANES) G_out[(size_t)w * ng + g] = sh.G[gtw_lds_word(w)];
+  for (uint32_t w = t; w < W_FP12; w += GTW_MILLER_LANES) G_out[(size_t)w * ng + g] = sh.G[gtw_lds_word(w)];
 }
 
-__global__ __launch_bounds__(GTW_LANES) void k_group_check(const uint32_t* S_in, const uint32_t* F_in, uint32_t ng,
+__global__ __launch_bounds__(GTW_MILLER_LANES) void k_group_check(const uint32_t* S_in, const uint32_t* F_in, uint32_t ng,
                                                            const uint32_t* G_in, const uint32_t* sel, uint8_t* ok) {
   __shared__ GtwLds sh;
   const uint32_t t = threadIdx.x;
   const uint32_t g = sel ? sel[blockIdx.x] : blockIdx.x;  // entry checked (S_in / F_in stride ng); verdict ok[blockIdx.x]
-  for (uint32_t w = t; w < W_FP12; w += GTW_LANES) {
+  for (uint32_t w = t; w < W_FP12; w += GTW_MILLER_LANES) {
     sh.F[gtw_lds_word(w)] = F_in[(size_t)w * ng + g];
     if (G_in) sh.G[gtw_lds_word(w)] = G_in[(size_t)w * ng + g];
   }
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(GTW_LANES) void k_group_check(const uint32_t* S_in,
   if (G_in) {
     gtw_mul<false>(sh.F, sh.F, sh.G, sh.S, t);
   } else if (sh.flag) {
-    gtw_miller_loop(sh.G, sh.QA, G1_GEN_X, G1_NEG_GEN_Y, sh.TB, sh.L, sh.S, t);
+    gtw_miller_loop(sh.G, sh.QA, G1_GEN_X, G1_NEG_GEN_Y, sh.TB, sh.L, sh.L1, sh.S, sh.S2, t);
     gtw_mul<false>(sh.F, sh.F, sh.G, sh.S, t);
   }
   gtw_final_exp(sh.F, sh.W, sh.S, t);
@@ -241,12 +241,14 @@ void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8
                         const uint32_t* sel, uint32_t n_sel, const uint32_t* G, bool exclusive) {
   const uint32_t n = sel ? n_sel : ng;
   if (n)
-    hipLaunchKernelGGL(k_group_check, dim3(n), dim3(GTW_LANES), exclusive ? exclusive_cu_lds(k_group_check) : 0, s, S,
+    hipLaunchKernelGGL(k_group_check, dim3(n), dim3(GTW_MILLER_LANES),
+                       exclusive ? exclusive_cu_lds<k_group_check>() : 0, s, S,
                        F, ng, G, sel, ok);
 }
 void launch_group_sig_miller(const uint32_t* S, uint32_t ng, uint32_t* G, hipStream_t s, bool exclusive) {
   if (ng)
-    hipLaunchKernelGGL(k_group_sig_miller, dim3(ng), dim3(GTW_LANES), exclusive ? exclusive_cu_lds(k_group_sig_miller) : 0,
+    hipLaunchKernelGGL(k_group_sig_miller, dim3(ng), dim3(GTW_MILLER_LANES),
+                       exclusive ? exclusive_cu_lds<k_group_sig_miller>() : 0,
                        s, S, ng, G);
 }
 void launch_range_combine(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,

@@ -81,8 +81,10 @@ STAGE_KERNEL_W(BLSGPU_WPE_HASH) void k_hash_clear(PipelineBuffers b) {
 }
 
 // The same clearing for small runs, latency first: one 16-lane group per message (g2_coop.hpp), four per workgroup;
-// the two [|z|] chains run as cooperative doublings, the additions and psi maps on the group's lane 0, the slots as
-// in k_hash_clear (the order of clear_cofactor_g2_slots).
+// the two [|z|] chains run as cooperative doublings and additions, and so do the six additions around them
+// (q0 + q1; B = A - psi(Q); A - Q; psi^2(2Q) - psi(Q); C; H = C + D) -- the lane-serial work left on the group's
+// lane 0 is psi, psi^2, one doubling and the operand moves.  HBM scratch per message: Q in h_q[2u], B in h_q[2u + 1],
+// A and then A - Q and C in h_jac[u] (all written and read by lane 0 only).
 #define HC_GROUPS (WAVE / G2C_LANES)
 __global__ __launch_bounds__(WAVE) void k_hash_clear_coop(PipelineBuffers b) {
   __shared__ uint32_t lds[HC_GROUPS * G2C_WORDS];
@@ -91,27 +93,53 @@ __global__ __launch_bounds__(WAVE) void k_hash_clear_coop(PipelineBuffers b) {
   const bool on = u < b.n_umsg;
   uint32_t* g = lds + grp * G2C_WORDS;
   const uint32_t qs = 2 * b.nm;
-  if (tg == 0 && on) {
-    const g2j Q = jac_add(ld_g2j(b.h_q, qs, 2 * u), ld_g2j(b.h_q, qs, 2 * u + 1));
-    st_g2j(b.h_q, qs, 2 * u, Q);
-    g2c_st_point(g, Q);
+  const bool l0 = tg == 0 && on;
+  if (l0) {
+    g2c_st_point(g, ld_g2j(b.h_q, qs, 2 * u));
+    g2c_st_q(g, ld_g2j(b.h_q, qs, 2 * u + 1));
   }
+  g2c_sync();
+  g2c_add(g, tg, on);  // Q = q0 + q1
+  if (l0) st_g2j(b.h_q, qs, 2 * u, g2c_ld_point(g));
   g2c_sync();
   // A = [|z|] Q
   g2c_mul_zabs(g, tg, on, [&] { return ld_g2j(b.h_q, qs, 2 * opaque_u32(u)); });
-  if (tg == 0 && on) {
-    const g2j A = g2c_ld_point(g), P = ld_g2j(b.h_q, qs, 2 * u);
-    const g2j psiP = g2_psi(P);
-    const g2j B = jac_add(A, jac_neg(psiP));
-    st_g2j(b.h_q, qs, 2 * u + 1, B);
-    st_g2j(b.h_jac, b.nm, u, jac_add(jac_add(g2_psi2(jac_dbl(P)), jac_neg(psiP)), jac_add(A, jac_neg(P))));  // C
-    g2c_st_point(g, B);
+  if (l0) {
+    st_g2j(b.h_jac, b.nm, u, g2c_ld_point(g));  // A
+    g2c_st_q(g, jac_neg(g2_psi(ld_g2j(b.h_q, qs, 2 * u))));
   }
   g2c_sync();
-  // D = [|z|] (A - psi(Q)); H = C + D
+  g2c_add(g, tg, on);  // B = A - psi(Q)
+  if (l0) {
+    st_g2j(b.h_q, qs, 2 * u + 1, g2c_ld_point(g));
+    g2c_st_point(g, ld_g2j(b.h_jac, b.nm, u));
+    g2c_st_q(g, jac_neg(ld_g2j(b.h_q, qs, 2 * u)));
+  }
+  g2c_sync();
+  g2c_add(g, tg, on);  // A - Q
+  if (l0) {
+    st_g2j(b.h_jac, b.nm, u, g2c_ld_point(g));
+    const g2j Q = ld_g2j(b.h_q, qs, 2 * u);
+    g2c_st_point(g, g2_psi2(jac_dbl(Q)));
+    g2c_st_q(g, jac_neg(g2_psi(Q)));
+  }
+  g2c_sync();
+  g2c_add(g, tg, on);  // psi^2(2Q) - psi(Q)
+  if (l0) g2c_st_q(g, ld_g2j(b.h_jac, b.nm, u));
+  g2c_sync();
+  g2c_add(g, tg, on);  // C = psi^2(2Q) - psi(Q) + A - Q
+  if (l0) {
+    st_g2j(b.h_jac, b.nm, u, g2c_ld_point(g));
+    g2c_st_point(g, ld_g2j(b.h_q, qs, 2 * u + 1));
+  }
+  g2c_sync();
+  // D = [|z|] B; H = C + D
   g2c_mul_zabs(g, tg, on, [&] { return ld_g2j(b.h_q, qs, 2 * opaque_u32(u) + 1); });
-  if (tg == 0 && on) {
-    const g2j H = jac_add(g2c_ld_point(g), ld_g2j(b.h_jac, b.nm, u));
+  if (l0) g2c_st_q(g, ld_g2j(b.h_jac, b.nm, u));
+  g2c_sync();
+  g2c_add(g, tg, on);
+  if (l0) {
+    const g2j H = g2c_ld_point(g);
     st_g2j(b.h_jac, b.nm, u, H);
     st_fp(b.h_norm, b.nm, u, 0, fp2_norm(H.z));
   }
@@ -126,7 +154,7 @@ void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s, bool coop) {
   hipLaunchKernelGGL(k_hash_map, grid_for(2 * b.n_umsg), dim3(WAVE), 0, s, b, b.inv_buf);
   if (coop)
     hipLaunchKernelGGL(k_hash_clear_coop, dim3((b.n_umsg + HC_GROUPS - 1) / HC_GROUPS), dim3(WAVE),
-                       BLSGPU_EXCLUSIVE_SMALL ? exclusive_cu_lds(k_hash_clear_coop) : 0, s, b);
+                       BLSGPU_EXCLUSIVE_SMALL ? exclusive_cu_lds<k_hash_clear_coop>() : 0, s, b);
   else
     hipLaunchKernelGGL(k_hash_clear, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
 }

@@ -91,7 +91,7 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc(PipelineBuffers b) {
 // k_miller_lines + k_miller_acc with one item per chunk, in ~1/6 of the time per pairing, at a fraction of the
 // lanes' efficiency; the runtime uses it only when the run's pairings fit the chip (runtime.cpp kCoopMaxItems).
 template <bool UNITS>
-__global__ __launch_bounds__(GTW_LANES) void k_miller_coop(PipelineBuffers b) {
+__global__ __launch_bounds__(GTW_MILLER_LANES) void k_miller_coop(PipelineBuffers b) {
   __shared__ GtwLds sh;
   const uint32_t c = blockIdx.x, t = threadIdx.x;
   if (c >= b.n_chunks) return;
@@ -110,12 +110,12 @@ __global__ __launch_bounds__(GTW_LANES) void k_miller_coop(PipelineBuffers b) {
     if (t < 4) lds_st(sh.QA, (int)t, ld_fp(b.h_aff, b.nm, m, (int)t * W_FP));
     const g1a P = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
     gtw_sync();
-    gtw_miller_loop(sh.G, sh.QA, P.x, P.y, sh.TB, sh.L, sh.S, t);
+    gtw_miller_loop(sh.G, sh.QA, P.x, P.y, sh.TB, sh.L, sh.L1, sh.S, sh.S2, t);
   } else {
     gtw_set_one(sh.G, t);
   }
   gtw_sync();
-  for (uint32_t w = t; w < W_FP12; w += GTW_LANES) b.f_chunk[(size_t)w * b.n + c] = sh.G[gtw_lds_word(w)];
+  for (uint32_t w = t; w < W_FP12; w += GTW_MILLER_LANES) b.f_chunk[(size_t)w * b.n + c] = sh.G[gtw_lds_word(w)];
 }
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
@@ -123,11 +123,11 @@ static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 void launch_miller_coop(const PipelineBuffers& b, bool units, hipStream_t s, bool exclusive) {
   if (!b.n_chunks) return;
   if (units)
-    hipLaunchKernelGGL(k_miller_coop<true>, dim3(b.n_chunks), dim3(GTW_LANES),
-                       exclusive ? exclusive_cu_lds(k_miller_coop<true>) : 0, s, b);
+    hipLaunchKernelGGL(k_miller_coop<true>, dim3(b.n_chunks), dim3(GTW_MILLER_LANES),
+                       exclusive ? exclusive_cu_lds<k_miller_coop<true>>() : 0, s, b);
   else
-    hipLaunchKernelGGL(k_miller_coop<false>, dim3(b.n_chunks), dim3(GTW_LANES),
-                       exclusive ? exclusive_cu_lds(k_miller_coop<false>) : 0, s, b);
+    hipLaunchKernelGGL(k_miller_coop<false>, dim3(b.n_chunks), dim3(GTW_MILLER_LANES),
+                       exclusive ? exclusive_cu_lds<k_miller_coop<false>>() : 0, s, b);
 }
 
 void launch_miller_lines(const PipelineBuffers& b, hipStream_t s) {

@@ -88,9 +88,8 @@ STAGE_KERNEL void k_msm_window(const uint32_t* range_slices, uint32_t n_ranges, 
 }
 
 // Horner passes on cooperative 16-lane groups (g2_coop.hpp): a workgroup of 128 lanes runs 4 ranges, group 2j the
-// S_a pass of range 4 blockIdx + j, group 2j + 1 its lambda S_b pass; the 28 doublings of a pass are cooperative
-// (3 product phases each), the 7 window additions and lambda run on the group's lane 0, then lane 0 of group 2j
-// adds its neighbour's lambda S_b from LDS.
+// S_a pass of range 4 blockIdx + j, group 2j + 1 its lambda S_b pass; the 28 doublings and 7 window additions of a
+// pass are cooperative (lambda on the group's lane 0), then group 2j adds its neighbour's lambda S_b the same way.
 #define MSM_H_LANES 128
 #define MSM_H_RANGES (MSM_H_LANES / G2C_LANES / 2)
 __global__ __launch_bounds__(MSM_H_LANES) void k_msm_horner(const uint32_t* W, uint32_t n_ranges, uint32_t* S) {
@@ -106,12 +105,16 @@ __global__ __launch_bounds__(MSM_H_LANES) void k_msm_horner(const uint32_t* W, u
   for (int k = MSM_WINDOWS / 2 - 2; k >= 0; k--) {
 #pragma unroll 1
     for (int d = 0; d < 4; d++) g2c_dbl(g, tg);
-    if (tg == 0 && on) g2c_st_point(g, jac_add(g2c_ld_point(g), ld_g2j(W, nw, base + (uint32_t)k)));
+    if (tg == 0 && on) g2c_st_q(g, ld_g2j(W, nw, base + (uint32_t)k));
     g2c_sync();
+    g2c_add(g, tg, on);
   }
   if (tg == 0 && on && part) g2c_st_point(g, endo_lambda(g2c_ld_point(g)));
   g2c_sync();
-  if (tg == 0 && on && !part) st_g2j(S, n_ranges, r, jac_add(g2c_ld_point(g), g2c_ld_point(g + G2C_WORDS)));
+  if (tg == 0 && on && !part) g2c_st_q(g, g2c_ld_point(g + G2C_WORDS));
+  g2c_sync();
+  g2c_add(g, tg, on && !part);
+  if (tg == 0 && on && !part) st_g2j(S, n_ranges, r, g2c_ld_point(g));
 }
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }

@@ -79,7 +79,7 @@ void launch_sig_decode(const PipelineBuffers& b, uint32_t n, hipStream_t s, bool
   hipLaunchKernelGGL(k_sig_decode, grid_for(n), dim3(WAVE), 0, s, b, n, !coop);
   if (coop)
     hipLaunchKernelGGL(k_sig_subgroup_coop, dim3((n + SG_GROUPS - 1) / SG_GROUPS), dim3(WAVE),
-                       BLSGPU_EXCLUSIVE_SMALL ? exclusive_cu_lds(k_sig_subgroup_coop) : 0, s, b, n);
+                       BLSGPU_EXCLUSIVE_SMALL ? exclusive_cu_lds<k_sig_subgroup_coop>() : 0, s, b, n);
 }
 void launch_sig_scale(const PipelineBuffers& b, uint32_t n, hipStream_t s, const uint32_t* list) {
   if (n) hipLaunchKernelGGL(k_sig_scale, grid_for(n), dim3(WAVE), 0, s, b, n, list);

@@ -6,6 +6,7 @@
 #include "../../lodestar_amd/csrc/msm.hpp"
 #include "../../lodestar_amd/csrc/lacc.hpp"
 #include "../../lodestar_amd/csrc/g2_coop.hpp"
+#include "../../lodestar_amd/csrc/gt_wave.hpp"
 
 #if defined(BLS_COUNT_OPS)
 unsigned long long bls_count_mul = 0, bls_count_sqr = 0, bls_count_half = 0;
@@ -151,6 +152,51 @@ int emu_g2c_mul_zabs(const uint8_t* p192, uint8_t* out192) {
   if (!jac_to_aff(r, o)) return 0;
   g2a_to_be192(o, out192);
   return 1;
+}
+// the cooperative addition (g2_coop.hpp g2c_add, phases lane by lane) of P and Q given affine (or infinity), each
+// lifted to Jacobian coordinates with a different Z; returns 0 for the point at infinity
+static g2j emu_lift(const g2a& a, int inf, uint32_t k) {
+  if (inf) return jac_infinity<fp2>();
+  fp zc0 = fp_zero(), zc1 = fp_one();
+  zc0.l[0] = k;  // Z = k + u (Montgomery limbs: any nonzero value will do)
+  const fp2 z = fp2_make(zc0, zc1), z2 = fp2_sqr(z);
+  g2j r;
+  r.x = fp2_mul(a.x, z2);
+  r.y = fp2_mul(a.y, fp2_mul(z2, z));
+  r.z = z;
+  return r;
+}
+int emu_g2c_add(const uint8_t* p192, int p_inf, const uint8_t* q192, int q_inf, uint8_t* out192) {
+  uint32_t g[G2C_WORDS] = {};
+  g2c_st_point(g, emu_lift(p_inf ? g2a{} : load_g2(p192), p_inf, 3));
+  g2c_st_q(g, emu_lift(q_inf ? g2a{} : load_g2(q192), q_inf, 5));
+  g2c_host_add(g);
+  g2a o;
+  if (!jac_to_aff(g2c_ld_point(g), o)) return 0;
+  g2a_to_be192(o, out192);
+  return 1;
+}
+// the cooperative Miller loop's phase schedule (gt_wave.hpp gtw_miller_schedule: the next step's line on lanes < 64, f
+// on lanes 64 .. 191), lanes run in turn within each phase
+void emu_gtw_miller(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) {
+  static uint32_t F[GTW_FP12], QA[4 * BLS_NL], TB[20 * BLS_NL], L0[GTW_FP12], L1[GTW_FP12], S[108 * BLS_NL],
+      S2[14 * BLS_NL];
+  const g1a P = load_g1(p96);
+  const g2a Q = load_g2(q192);
+  lds_st(QA, 0, Q.x.c0);
+  lds_st(QA, 1, Q.x.c1);
+  lds_st(QA, 2, Q.y.c0);
+  lds_st(QA, 3, Q.y.c1);
+  gtw_miller_schedule(
+      [&](auto&& phase) {
+        for (uint32_t t = 0; t < GTW_MILLER_LANES; t++) phase(t);
+      },
+      F, QA, P.x, P.y, TB, L0, L1, S, S2);
+  // w-basis coefficient k -> tower slot (c0.c0, c1.c0, c0.c1, c1.c1, c0.c2, c1.c2)[k]
+  fp12 f;
+  fp2* slot[6] = {&f.c0.c0, &f.c1.c0, &f.c0.c1, &f.c1.c1, &f.c0.c2, &f.c1.c2};
+  for (int k = 0; k < 6; k++) *slot[k] = fp2_make(lds_ld(F, 2 * k), lds_ld(F, 2 * k + 1));
+  store12(f, out576);
 }
 #if defined(BLS_COUNT_OPS)
 // bucket MSM over n distinct points (the count covers the MSM only, not the point loads)

@@ -164,6 +164,9 @@ def test_miller_and_final_exp():
     o2 = buf(576)
     L.emu_final_exp(f12b(f), o2)
     assert b2f12(o2.raw) == bls.final_exp(f)
+    o4 = buf(576)  # the cooperative loop's phase schedule (gt_wave.hpp: f and the next line on separate waves)
+    L.emu_gtw_miller(g1b(Pp), g2b(Q), o4)
+    assert b2f12(o4.raw) == f
 
 
 def test_sig_decode_classes():
@@ -366,9 +369,35 @@ def test_lacc_fin_and_lazy_operands():
         assert v % P == (x0 + x1) * (x0 - x1) * R_INV % P, trial
 
 
+def test_cooperative_g2_addition():
+    """g2_coop.hpp g2c_add: the cooperative Jacobian addition (five product phases + five recombinations, operands
+    with different Z), phases run lane by lane on the host, against the oracle's affine sum -- generic pairs, points
+    outside G2, and the exceptional cases jac_add handles (P = Q, P = -Q, an infinite operand)."""
+    L = lib()
+    o = buf(192)
+    r2 = random.Random(909)
+    pts = [bls.g2_mul(bls.G2_GEN, r2.randrange(1, bls.R)) for _ in range(4)]
+    while len(pts) < 6:  # points of E2 not in G2
+        x = (r2.randrange(P), r2.randrange(P))
+        y = bls.f2sqrt(bls.f2add(bls.f2mul(bls.f2sqr(x), x), bls.B2))
+        if y:
+            pts.append((x, y))
+    neg = lambda q: (q[0], bls.f2neg(q[1]))
+    cases = [(pts[i], pts[j]) for i in range(6) for j in range(6) if i != j]
+    cases += [(q, q) for q in pts] + [(q, neg(q)) for q in pts] + [(None, pts[0]), (pts[1], None), (None, None)]
+    for p_, q_ in cases:
+        want = bls.g2_add(p_, q_)
+        rc = L.emu_g2c_add(g2b(p_) if p_ else bytes(192), int(p_ is None), g2b(q_) if q_ else bytes(192),
+                           int(q_ is None), o)
+        if want is None:
+            assert rc == 0
+        else:
+            assert rc == 1 and b2g2(o.raw) == want
+
+
 def test_cooperative_g2_doubling_chain():
     """g2_coop.hpp: the [|z|] chain as the 16-lane groups run it (three product phases + two recombinations per
-    doubling, additions on lane 0), phases executed lane by lane on the host, against the oracle's [|z|]P -- on G2
+    doubling, cooperative additions), phases executed lane by lane on the host, against the oracle's [|z|]P -- on G2
     points and on points of E2 outside G2 (the cofactor clearing's inputs)."""
     L = lib()
     o = buf(192)
