@@ -120,18 +120,21 @@ __global__ __launch_bounds__(GTW_MILLER_LANES) void k_group_sig_miller(const uin
   for (uint32_t w = t; w < W_FP12; w += GTW_MILLER_LANES) G_out[(size_t)w * ng + g] = sh.G[gtw_lds_word(w)];
 }
 
-__global__ __launch_bounds__(GTW_MILLER_LANES) void k_group_check(const uint32_t* S_in, const uint32_t* F_in, uint32_t ng,
-                                                           const uint32_t* G_in, const uint32_t* sel, uint8_t* ok) {
+// MILLER: G_in is null, the kernel runs MillerLoop(-g1, S) itself (three waves, gtw_miller_loop); otherwise two
+template <bool MILLER>
+__global__ __launch_bounds__(MILLER ? GTW_MILLER_LANES : GTW_LANES) void k_group_check(
+    const uint32_t* S_in, const uint32_t* F_in, uint32_t ng, const uint32_t* G_in, const uint32_t* sel, uint8_t* ok) {
+  constexpr uint32_t NT = MILLER ? GTW_MILLER_LANES : GTW_LANES;
   __shared__ GtwLds sh;
   const uint32_t t = threadIdx.x;
   const uint32_t g = sel ? sel[blockIdx.x] : blockIdx.x;  // entry checked (S_in / F_in stride ng); verdict ok[blockIdx.x]
-  for (uint32_t w = t; w < W_FP12; w += GTW_MILLER_LANES) {
+  for (uint32_t w = t; w < W_FP12; w += NT) {
     sh.F[gtw_lds_word(w)] = F_in[(size_t)w * ng + g];
-    if (G_in) sh.G[gtw_lds_word(w)] = G_in[(size_t)w * ng + g];
+    if (!MILLER) sh.G[gtw_lds_word(w)] = G_in[(size_t)w * ng + g];
   }
-  if (!G_in) gtw_load_S(sh, S_in, ng, g, t);
+  if (MILLER) gtw_load_S(sh, S_in, ng, g, t);
   gtw_sync();
-  if (G_in) {
+  if (!MILLER) {
     gtw_mul<false>(sh.F, sh.F, sh.G, sh.S, t);
   } else if (sh.flag) {
     gtw_miller_loop(sh.G, sh.QA, G1_GEN_X, G1_NEG_GEN_Y, sh.TB, sh.L, sh.L1, sh.S, sh.S2, t);
@@ -240,10 +243,13 @@ void launch_group_tree(const PipelineBuffers& b, const uint32_t* f_ranges, uint3
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s,
                         const uint32_t* sel, uint32_t n_sel, const uint32_t* G, bool exclusive) {
   const uint32_t n = sel ? n_sel : ng;
-  if (n)
-    hipLaunchKernelGGL(k_group_check, dim3(n), dim3(GTW_MILLER_LANES),
-                       exclusive ? exclusive_cu_lds<k_group_check>() : 0, s, S,
-                       F, ng, G, sel, ok);
+  if (!n) return;
+  if (G)
+    hipLaunchKernelGGL(k_group_check<false>, dim3(n), dim3(GTW_LANES),
+                       exclusive ? exclusive_cu_lds<k_group_check<false>>() : 0, s, S, F, ng, G, sel, ok);
+  else
+    hipLaunchKernelGGL(k_group_check<true>, dim3(n), dim3(GTW_MILLER_LANES),
+                       exclusive ? exclusive_cu_lds<k_group_check<true>>() : 0, s, S, F, ng, G, sel, ok);
 }
 void launch_group_sig_miller(const uint32_t* S, uint32_t ng, uint32_t* G, hipStream_t s, bool exclusive) {
   if (ng)
