@@ -78,16 +78,6 @@ BLS_INL void g2c_dbl_p2(uint32_t* g, uint32_t tg) {
     lds_st(g, G2C_S + 7 + tg, fp_mul(X, Y));
   }
 }
-// lacc of sum_j c_j S[j] over the products (coefficients -8..6)
-BLS_INL void g2c_lacc_term(lacc& a, const uint32_t* g, int slot, int coef) {
-  const fp v = lds_ld(g, slot);
-  for (int k = 0; k < (coef < 0 ? -coef : coef); k++) {
-    if (coef > 0)
-      lacc_add(a, v);
-    else
-      lacc_sub(a, v);
-  }
-}
 BLS_INL void g2c_dbl_r1(uint32_t* g, uint32_t tg) {
   if (tg < 6) {
     const int c = (int)(tg & 1);
@@ -96,25 +86,25 @@ BLS_INL void g2c_dbl_r1(uint32_t* g, uint32_t tg) {
     lacc_init(a);
     int dst;
     if (tg < 2) {  // W = 6T - 6A - 6C - F
-      g2c_lacc_term(a, g, G2C_S + 9 + c, 6);
-      g2c_lacc_term(a, g, G2C_S + c, -6);
-      g2c_lacc_term(a, g, G2C_S + 7 + c, -6);
-      g2c_lacc_term(a, g, G2C_S + 11 + c, -1);
+      lacc_term(a, g, G2C_S + 9 + c, 6);
+      lacc_term(a, g, G2C_S + c, -6);
+      lacc_term(a, g, G2C_S + 7 + c, -6);
+      lacc_term(a, g, G2C_S + 11 + c, -1);
       dst = G2C_W + c;
     } else if (tg < 4) {  // X3 = F - 4T + 4A + 4C
-      g2c_lacc_term(a, g, G2C_S + 11 + c, 1);
-      g2c_lacc_term(a, g, G2C_S + 9 + c, -4);
-      g2c_lacc_term(a, g, G2C_S + c, 4);
-      g2c_lacc_term(a, g, G2C_S + 7 + c, 4);
+      lacc_term(a, g, G2C_S + 11 + c, 1);
+      lacc_term(a, g, G2C_S + 9 + c, -4);
+      lacc_term(a, g, G2C_S + c, 4);
+      lacc_term(a, g, G2C_S + 7 + c, 4);
       dst = G2C_R + c;
     } else {  // Z3 = 2 Y Z: 2 (K0 - K1) + 2 (K2 - K0 - K1) u
       if (c == 0) {
-        g2c_lacc_term(a, g, G2C_S + 4, 2);
-        g2c_lacc_term(a, g, G2C_S + 5, -2);
+        lacc_term(a, g, G2C_S + 4, 2);
+        lacc_term(a, g, G2C_S + 5, -2);
       } else {
-        g2c_lacc_term(a, g, G2C_S + 6, 2);
-        g2c_lacc_term(a, g, G2C_S + 4, -2);
-        g2c_lacc_term(a, g, G2C_S + 5, -2);
+        lacc_term(a, g, G2C_S + 6, 2);
+        lacc_term(a, g, G2C_S + 4, -2);
+        lacc_term(a, g, G2C_S + 5, -2);
       }
       dst = G2C_R + 4 + c;
     }
@@ -135,14 +125,14 @@ BLS_INL void g2c_dbl_r2(uint32_t* g, uint32_t tg) {
     lacc a;
     lacc_init(a);
     if (c == 0) {  // P0 - P1 - 8 C0
-      g2c_lacc_term(a, g, G2C_S + 13, 1);
-      g2c_lacc_term(a, g, G2C_S + 14, -1);
+      lacc_term(a, g, G2C_S + 13, 1);
+      lacc_term(a, g, G2C_S + 14, -1);
     } else {  // P2 - P0 - P1 - 8 C1
-      g2c_lacc_term(a, g, G2C_S + 15, 1);
-      g2c_lacc_term(a, g, G2C_S + 13, -1);
-      g2c_lacc_term(a, g, G2C_S + 14, -1);
+      lacc_term(a, g, G2C_S + 15, 1);
+      lacc_term(a, g, G2C_S + 13, -1);
+      lacc_term(a, g, G2C_S + 14, -1);
     }
-    g2c_lacc_term(a, g, G2C_S + 7 + c, -8);
+    lacc_term(a, g, G2C_S + 7 + c, -8);
     lds_st(g, G2C_R + 2 + c, lacc_fin(a));
   }
 }
@@ -162,17 +152,6 @@ BLS_INL void g2c_dbl_r2(uint32_t* g, uint32_t tg) {
 // cases (an infinite operand, H = 0) are detected by the writer lanes of R5 from the operands, which stay in place
 // until then, and lane 0 writes jac_add's result instead: every group passes the same barriers.
 #define G2C_A 30
-// Karatsuba component c of a product whose three products sit at slots k .. k + 2
-BLS_INL void g2c_kara_term(lacc& a, const uint32_t* g, int k, int c, int coef) {
-  if (c == 0) {  // P0 - P1
-    g2c_lacc_term(a, g, k, coef);
-    g2c_lacc_term(a, g, k + 1, -coef);
-  } else {  // P2 - P0 - P1
-    g2c_lacc_term(a, g, k + 2, coef);
-    g2c_lacc_term(a, g, k, -coef);
-    g2c_lacc_term(a, g, k + 1, -coef);
-  }
-}
 BLS_INL void g2c_add_p1(uint32_t* g, uint32_t tg) {
   if (tg < 12) {
     fp X, Y;
@@ -198,13 +177,13 @@ BLS_INL void g2c_add_r1(uint32_t* g, uint32_t tg) {
     lacc a;
     lacc_init(a);
     if (tg < 2) {
-      g2c_kara_term(a, g, G2C_A + 4, c, 1);  // Y1 Z2
+      lacc_kara(a, g, G2C_A + 4, c, 1);  // Y1 Z2
     } else if (tg < 4) {
-      g2c_kara_term(a, g, G2C_A + 7, c, 1);  // Y2 Z1
+      lacc_kara(a, g, G2C_A + 7, c, 1);  // Y2 Z1
     } else {  // (Z1 + Z2)^2 - Z1Z1 - Z2Z2 (the squares' components are products)
-      g2c_lacc_term(a, g, G2C_A + 10 + c, 1);
-      g2c_lacc_term(a, g, G2C_A + c, -1);
-      g2c_lacc_term(a, g, G2C_A + 2 + c, -1);
+      lacc_term(a, g, G2C_A + 10 + c, 1);
+      lacc_term(a, g, G2C_A + c, -1);
+      lacc_term(a, g, G2C_A + 2 + c, -1);
     }
     lds_st(g, G2C_A + 12 + tg, lacc_fin(a));
   }
@@ -227,13 +206,13 @@ BLS_INL void g2c_add_r2(uint32_t* g, uint32_t tg) {
     lacc a;
     lacc_init(a);
     if (k == 0) {  // H
-      g2c_kara_term(a, g, U2, c, 1);
-      g2c_kara_term(a, g, U1, c, -1);
+      lacc_kara(a, g, U2, c, 1);
+      lacc_kara(a, g, U1, c, -1);
     } else if (k == 1) {  // r
-      g2c_kara_term(a, g, S2, c, 2);
-      g2c_kara_term(a, g, S1, c, -2);
+      lacc_kara(a, g, S2, c, 2);
+      lacc_kara(a, g, S1, c, -2);
     } else {  // U1, S1
-      g2c_kara_term(a, g, k == 2 ? U1 : S1, c, 1);
+      lacc_kara(a, g, k == 2 ? U1 : S1, c, 1);
     }
     lds_st(g, G2C_A + 30 + tg, lacc_fin(a));
   }
@@ -261,7 +240,7 @@ BLS_INL void g2c_add_r3(uint32_t* g, uint32_t tg) {
   if (tg < 2) {
     lacc a;
     lacc_init(a);
-    g2c_kara_term(a, g, G2C_A + 4, (int)tg, 1);
+    lacc_kara(a, g, G2C_A + 4, (int)tg, 1);
     lds_st(g, G2C_A + 7 + tg, lacc_fin(a));  // Z3: 37, 38
   }
 }
@@ -280,15 +259,15 @@ BLS_INL void g2c_add_r4(uint32_t* g, uint32_t tg) {
     lacc a;
     lacc_init(a);
     if (k == 0) {  // X3 = r^2 - J - 2V
-      g2c_lacc_term(a, g, G2C_A + 2 + c, 1);
-      g2c_kara_term(a, g, J, c, -1);
-      g2c_kara_term(a, g, V, c, -2);
+      lacc_term(a, g, G2C_A + 2 + c, 1);
+      lacc_kara(a, g, J, c, -1);
+      lacc_kara(a, g, V, c, -2);
     } else if (k == 1) {  // W = 3V - r^2 + J
-      g2c_kara_term(a, g, V, c, 3);
-      g2c_lacc_term(a, g, G2C_A + 2 + c, -1);
-      g2c_kara_term(a, g, J, c, 1);
+      lacc_kara(a, g, V, c, 3);
+      lacc_term(a, g, G2C_A + 2 + c, -1);
+      lacc_kara(a, g, J, c, 1);
     } else {  // J
-      g2c_kara_term(a, g, J, c, 1);
+      lacc_kara(a, g, J, c, 1);
     }
     lds_st(g, G2C_A + 24 + tg, lacc_fin(a));  // X3 54, 55; W 56, 57; J 58, 59
   }
@@ -323,8 +302,8 @@ BLS_INL void g2c_add_r5(const uint32_t* g, uint32_t* w, uint32_t tg, bool exc) {
     const int c = (int)tg - 2;
     lacc a;
     lacc_init(a);
-    g2c_kara_term(a, g, G2C_A + 9, c, 1);
-    g2c_kara_term(a, g, G2C_A + 12, c, -2);
+    lacc_kara(a, g, G2C_A + 9, c, 1);
+    lacc_kara(a, g, G2C_A + 12, c, -2);
     v = lacc_fin(a);
   } else {
     v = lds_ld(g, G2C_A + 7 + (tg - 4));  // Z3
@@ -386,6 +365,7 @@ __device__ void g2c_mul_zabs(uint32_t* g, uint32_t tg, bool on, LoadP loadP) {
     }
   }
 }
+
 #else
 // host model of the same schedules (tests): phases lane by lane, a group of one
 static void g2c_host_add(uint32_t* g) {

@@ -257,10 +257,17 @@ __device__ void gtw_pow_z(uint32_t* Y, const uint32_t* X, uint32_t* S, uint32_t 
 
 __device__ void gtw_final_exp(uint32_t* F, uint32_t* W, uint32_t* S, uint32_t t) {
   uint32_t *U = W, *V = W + GTW_FP12, *M = W + 2 * GTW_FP12, *T = W + 3 * GTW_FP12, *X = W + 4 * GTW_FP12;
-  if (t == 0) gtw_from_reg(U, fp12_inv(gtw_to_reg(F)));
-  gtw_sync();
+  // f1 = conj(f) / f = conj(f)^2 / (f conj(f)), where f conj(f) = a0^2 - v a1^2 lies in Fp6: the two Fp12
+  // products are cooperative and lane 0 inverts only an Fp6 (the lane-0 Fp12 inverse took 271 us in the probe)
   gtw_conj(V, F, t);
-  gtw_mul<false>(V, V, U, S, t);  // f1 = conj(f) / f
+  gtw_mul<false>(U, F, V, S, t);  // f conj(f): odd w-coefficients 0
+  gtw_mul<false>(V, V, V, S, t);  // conj(f)^2
+  if (t == 0) {
+    const fp12 n = gtw_to_reg(U);
+    gtw_from_reg(U, fp12_make(fp6_inv(n.c0), fp6_zero()));
+  }
+  gtw_sync();
+  gtw_mul<false>(V, V, U, S, t);  // f1
   gtw_frob(U, V, 2, t);
   gtw_mul<false>(M, U, V, S, t);  // m = f1^(p^2) f1
   gtw_pow_z(U, M, S, t);
@@ -291,12 +298,11 @@ __device__ void gtw_final_exp(uint32_t* F, uint32_t* W, uint32_t* S, uint32_t t)
 // (14 Fp).  L0 / L1: Fp12-layout line buffers (w-coefficients 0, 2, 3 used), S2: the T chain's products.
 //
 // Three waves (GTW_MILLER_LANES): waves 1-2 update f (square: 108 products + recombination; times the sparse
-// line: 54 + recombination -- four barrier-separated phases per step) while wave 0 computes the NEXT step's line
-// from T in the same four phases (doubling: products, linear combination, products, linear combination; addition:
-// lane-serial in the first phase, on lane 0: its Fp2 products use fp2_mul's per-lane LDS slot, tower.hpp, which
-// covers lanes 0 .. 127 only -- the f lanes use none).  The line chain depends only on T, so it leaves the critical path of the f
-// chain; the line of step s sits in L[s & 1].  Divergent lanes of ONE wave would run both paths in turn, hence a
-// wave of its own.
+// line: 54 + recombination) while wave 0 runs the T chain that produces the lines (cooperative doubling and
+// addition steps: products, linear combinations, ...), up to two lines ahead (gtw_miller_schedule).  The line
+// chain depends only on T, so it leaves the critical path of the f chain (divergent lanes of ONE wave would run both
+// paths in turn, hence a wave of its own).  The T chain's Fp products are all fp_mul: fp2_mul's per-lane LDS argument
+// slot (tower.hpp) covers lanes 0 .. 127 only.
 // ---------------------------------------------------------------------------------------------------
 #define GTW_MILLER_LANES (GTW_LANES + 64)
 
@@ -383,104 +389,227 @@ BLS_INL void gtw_dbl_p4(uint32_t* TB, uint32_t* L, const uint32_t* S, uint32_t t
   }
 }
 
-BLS_INL void gtw_add_step_lane(uint32_t* TB, const uint32_t* QA, uint32_t* L, const fp& xP, const fp& yP,
-                               uint32_t t) {
-  if (t == 0) {
-    g2proj T;
-    T.x = fp2_make(lds_ld(TB, 0), lds_ld(TB, 1));
-    T.y = fp2_make(lds_ld(TB, 2), lds_ld(TB, 3));
-    T.z = fp2_make(lds_ld(TB, 4), lds_ld(TB, 5));
-    g2a Q;
-    Q.x = fp2_make(lds_ld(QA, 0), lds_ld(QA, 1));
-    Q.y = fp2_make(lds_ld(QA, 2), lds_ld(QA, 3));
-    fp2 l0, l1, l4;
-    miller_add_step(T, Q, xP, yP, l0, l1, l4);
-    lds_st(TB, 0, T.x.c0);
-    lds_st(TB, 1, T.x.c1);
-    lds_st(TB, 2, T.y.c0);
-    lds_st(TB, 3, T.y.c1);
-    lds_st(TB, 4, T.z.c0);
-    lds_st(TB, 5, T.z.c1);
-    lds_st(L, 0, l0.c0);
-    lds_st(L, 1, l0.c1);
-    lds_st(L, 4, l1.c0);
-    lds_st(L, 5, l1.c1);
-    lds_st(L, 6, l4.c0);
-    lds_st(L, 7, l4.c1);
+// addition step phases (mixed addition T + Q with the chord line; the formulas of pairing.hpp miller_add_step), lane
+// t of the T-chain wave; products in S (28 slots), sums in D = TB + 6 (theta 0-1, lambda 2-3, E 4-5, H 6-7, G - H 8-9)
+BLS_INL void gtw_add_q1(const uint32_t* TB, const uint32_t* QA, uint32_t* S, uint32_t t) {  // Qy Tz, Qx Tz
+  if (t < 6) {
+    const int q = t < 3 ? 2 : 0, c = (int)t % 3;
+    fp X, Y;
+    kara_operands(lds_ld(QA, q), lds_ld(QA, q + 1), lds_ld(TB, 4), lds_ld(TB, 5), c, X, Y);
+    lds_st(S, (int)t, fp_mul(X, Y));
+  }
+}
+BLS_INL void gtw_add_r1(uint32_t* TB, const uint32_t* S, uint32_t t) {  // theta = Ty - Qy Tz, lambda = Tx - Qx Tz
+  if (t < 4) {
+    const int k = (int)t >> 1, c = (int)t & 1;
+    lacc a;
+    lacc_init(a);
+    lacc_term(a, TB, k ? c : 2 + c, 1);
+    lacc_kara(a, S, k ? 3 : 0, c, -1);
+    lds_st(TB + 6 * BLS_NL, (int)t, lacc_fin(a));
+  }
+}
+BLS_INL void gtw_add_q2(const uint32_t* TB, const uint32_t* QA, uint32_t* S, const fp& xP, const fp& yP, uint32_t t) {
+  const uint32_t* D = TB + 6 * BLS_NL;
+  if (t < 14) {  // C = theta^2 (2), D = lambda^2 (2), theta Qx (3), lambda Qy (3), theta xP (2), lambda yP (2)
+    fp X, Y;
+    if (t < 4) {
+      const int k = t < 2 ? 0 : 2;
+      sqr_operands(lds_ld(D, k), lds_ld(D, k + 1), (int)t & 1, X, Y);
+    } else if (t < 10) {
+      const int k = t < 7 ? 0 : 2, q = t < 7 ? 0 : 2, c = t < 7 ? (int)t - 4 : (int)t - 7;
+      kara_operands(lds_ld(D, k), lds_ld(D, k + 1), lds_ld(QA, q), lds_ld(QA, q + 1), c, X, Y);
+    } else {
+      X = lds_ld(D, t < 12 ? (int)t - 10 : 2 + (int)t - 12);
+      Y = t < 12 ? xP : yP;
+    }
+    lds_st(S, (int)t, fp_mul(X, Y));
+  }
+}
+BLS_INL void gtw_add_r2(const uint32_t* S, uint32_t* L, uint32_t t) {  // the line: l0, l1 = -theta xP, l4 = lambda yP
+  if (t < 6) {
+    const int c = (int)t & 1;
+    if (t < 2) {
+      lacc a;
+      lacc_init(a);
+      lacc_kara(a, S, 4, c, 1);
+      lacc_kara(a, S, 7, c, -1);
+      lds_st(L, c, lacc_fin(a));
+    } else if (t < 4) {
+      lds_st(L, 4 + c, fp_neg(lds_ld(S, 10 + c)));
+    } else {
+      lds_st(L, 6 + c, lds_ld(S, 12 + c));
+    }
+  }
+}
+BLS_INL void gtw_add_q3(const uint32_t* TB, uint32_t* S, uint32_t t) {  // E = lambda D, F = Tz C, G = Tx D
+  const uint32_t* D = TB + 6 * BLS_NL;
+  if (t < 9) {
+    const int m = (int)t / 3, c = (int)t % 3;
+    fp a0, a1;
+    if (m == 0) {
+      a0 = lds_ld(D, 2);
+      a1 = lds_ld(D, 3);
+    } else {
+      a0 = lds_ld(TB, m == 1 ? 4 : 0);
+      a1 = lds_ld(TB, m == 1 ? 5 : 1);
+    }
+    const int b = m == 1 ? 0 : 2;  // C = S0, S1; D = S2, S3 (squares: the products are the components)
+    fp X, Y;
+    kara_operands(a0, a1, lds_ld(S, b), lds_ld(S, b + 1), c, X, Y);
+    lds_st(S, 14 + (int)t, fp_mul(X, Y));
+  }
+}
+BLS_INL void gtw_add_r3(uint32_t* TB, const uint32_t* S, uint32_t t) {  // E, H = E + F - 2G, G - H = 3G - E - F
+  if (t < 6) {
+    const int k = (int)t >> 1, c = (int)t & 1;
+    lacc a;
+    lacc_init(a);
+    if (k == 0) {
+      lacc_kara(a, S, 14, c, 1);
+    } else if (k == 1) {
+      lacc_kara(a, S, 14, c, 1);
+      lacc_kara(a, S, 17, c, 1);
+      lacc_kara(a, S, 20, c, -2);
+    } else {
+      lacc_kara(a, S, 20, c, 3);
+      lacc_kara(a, S, 14, c, -1);
+      lacc_kara(a, S, 17, c, -1);
+    }
+    lds_st(TB + 6 * BLS_NL, 4 + (int)t, lacc_fin(a));
+  }
+}
+BLS_INL void gtw_add_q4(const uint32_t* TB, uint32_t* S, uint32_t t) {  // lambda H, theta (G - H), Ty E, Tz E
+  const uint32_t* D = TB + 6 * BLS_NL;
+  if (t < 12) {
+    const int m = (int)t / 3, c = (int)t % 3;
+    const uint32_t* ab = m < 2 ? D : TB;
+    const int ka = m == 0 ? 2 : m == 1 ? 0 : m == 2 ? 2 : 4;
+    const int kb = m == 0 ? 6 : m == 1 ? 8 : 4;
+    fp X, Y;
+    kara_operands(lds_ld(ab, ka), lds_ld(ab, ka + 1), lds_ld(D, kb), lds_ld(D, kb + 1), c, X, Y);
+    lds_st(S, (int)t, fp_mul(X, Y));
+  }
+}
+BLS_INL void gtw_add_r4(uint32_t* TB, const uint32_t* S, uint32_t t) {  // T = (lambda H, theta (G - H) - Ty E, Tz E)
+  if (t < 6) {
+    const int k = (int)t >> 1, c = (int)t & 1;
+    lacc a;
+    lacc_init(a);
+    if (k == 1) {
+      lacc_kara(a, S, 3, c, 1);
+      lacc_kara(a, S, 6, c, -1);
+    } else {
+      lacc_kara(a, S, k == 0 ? 0 : 9, c, 1);
+    }
+    lds_st(TB, (int)t, lacc_fin(a));
   }
 }
 
 // The loop as a schedule of phases: run(f) executes phase f for every lane of the workgroup (on the device: the
 // calling lane, then a barrier; in the host model, tests/native/emu.cpp: lanes 0 .. GTW_MILLER_LANES - 1 in turn --
 // within a phase no lane reads what another writes).
+//
+// The T chain (wave 0) and the f chain (waves 1-2) are two programs stepped once per phase:
+//   T, per step: a doubling in 4 phases (products, sums, products, sums) or an addition in 8 (gtw_add_q1 .. r4);
+//      its line is complete after the step's 4th phase; it starts step t only when the f chain has consumed line
+//      t - 2 (two line buffers, L[t & 1]);
+//   f, per step: square (products, recombination; not at step 0 or after an addition step) then times the sparse
+//      line (products, recombination); the line products wait, idle, until the T chain has completed that line.
+// The f chain runs 4 phases per doubling step and 2 per addition step, the T chain 4 and 8: the T chain, ahead by
+// up to two lines, absorbs the five additions' extra phases instead of stalling the f chain for lane-serial ones.
 template <class Run>
 BLS_INL void gtw_miller_schedule(Run&& run, uint32_t* F, const uint32_t* QA, const fp& xP, const fp& yP, uint32_t* TB,
                                  uint32_t* L0, uint32_t* L1, uint32_t* S, uint32_t* S2) {
   constexpr uint32_t TW = 64;  // lanes < TW: the T-chain wave; lane TW + i: f-lane i
+  constexpr int NSTEPS = 68;
+  // step kinds: step 0 doubles for bit 62; after the doubling for bit b an addition if bit b of |z| is set
+  uint64_t add_lo = 0, add_hi = 0;  // bit s: step s is an addition
+  {
+    int st = 0;
+    for (int bit = 62; bit >= 0; bit--) {
+      st++;  // the doubling
+      if ((BLS_Z_ABS >> bit) & 1ull) {
+        if (st < 64)
+          add_lo |= 1ull << st;
+        else
+          add_hi |= 1ull << (st - 64);
+        st++;
+      }
+    }
+  }
+  auto is_add = [&](int st) { return st < 64 ? ((add_lo >> st) & 1ull) != 0 : ((add_hi >> (st - 64)) & 1ull) != 0; };
   run([&](uint32_t t) {
     if (t < 6) lds_st(TB, (int)t, t < 4 ? lds_ld(QA, (int)t) : (t == 4 ? FP_ONE : fp_zero()));
     if (t < 12) lds_st(F, (int)t, t == 0 ? FP_ONE : fp_zero());
   });
-  // the line of step 0 (a doubling)
-  run([&](uint32_t t) {
-    if (t < TW) gtw_dbl_p1(TB, S2, t);
-  });
-  run([&](uint32_t t) {
-    if (t < TW) gtw_dbl_p2(TB, L0, S2, t);
-  });
-  run([&](uint32_t t) {
-    if (t < TW) gtw_dbl_p3(TB, S2, xP, yP, t);
-  });
-  run([&](uint32_t t) {
-    if (t < TW) gtw_dbl_p4(TB, L0, S2, t);
-  });
-  int bit = 61;
-  bool add_next = (BLS_Z_ABS >> 62) & 1ull, cur_add = false;
+  int ts = 0, tp = 0;  // T chain: step, phase within it
+  int fs = 0, fp_ = 0;  // f chain: step, phase within it
+  int lines_done = 0, lines_used = 0;
 #pragma unroll 1
-  for (int s = 0; s < 68; s++) {
-    uint32_t* cur = (s & 1) ? L1 : L0;
-    uint32_t* nxt = (s & 1) ? L0 : L1;
-    const bool more = s + 1 < 68, next_add = add_next;
-    if (more) {
-      if (next_add) {
-        add_next = false;
-      } else {
-        add_next = (BLS_Z_ABS >> bit) & 1ull;
-        bit--;
+  while (fs < NSTEPS) {
+    // T: may start step ts once line ts - 2 has been consumed
+    const bool t_on = ts < NSTEPS && (tp > 0 || ts < lines_used + 2);
+    const bool t_add = ts < NSTEPS && is_add(ts);
+    uint32_t* tl = (ts & 1) ? L1 : L0;
+    // f: the phases of step fs (a doubling step after step 0: 4, else 2; the first two square f)
+    const bool f_sq_step = fs > 0 && !is_add(fs);
+    const int f_ph = f_sq_step ? fp_ : fp_ + 2;  // 0 square products, 1 square sums, 2 line products, 3 line sums
+    const bool f_on = f_ph != 2 || lines_done > fs;
+    const uint32_t* fl = (fs & 1) ? L1 : L0;
+    const int tpc = tp;
+    run([&](uint32_t t) {
+      if (t < TW) {
+        if (!t_on) return;
+        if (!t_add) {
+          if (tpc == 0)
+            gtw_dbl_p1(TB, S2, t);
+          else if (tpc == 1)
+            gtw_dbl_p2(TB, tl, S2, t);
+          else if (tpc == 2)
+            gtw_dbl_p3(TB, S2, xP, yP, t);
+          else
+            gtw_dbl_p4(TB, tl, S2, t);
+        } else {
+          switch (tpc) {
+            case 0: gtw_add_q1(TB, QA, S2, t); break;
+            case 1: gtw_add_r1(TB, S2, t); break;
+            case 2: gtw_add_q2(TB, QA, S2, xP, yP, t); break;
+            case 3: gtw_add_r2(S2, tl, t); break;
+            case 4: gtw_add_q3(TB, S2, t); break;
+            case 5: gtw_add_r3(TB, S2, t); break;
+            case 6: gtw_add_q4(TB, S2, t); break;
+            default: gtw_add_r4(TB, S2, t); break;
+          }
+        }
+      } else if (f_on) {
+        const uint32_t u = t - TW;
+        if (f_ph == 0)
+          gtw_mul_prod<false>(F, F, S, u);
+        else if (f_ph == 1)
+          gtw_mul_rec<false>(F, S, u);
+        else if (f_ph == 2)
+          gtw_mul_prod<true>(F, fl, S, u);
+        else
+          gtw_mul_rec<true>(F, S, u);
+      }
+    });
+    if (t_on) {
+      if (tp == 3) lines_done = ts + 1;
+      if (++tp == (t_add ? 8 : 4)) {
+        ts++;
+        tp = 0;
       }
     }
-    const bool sq = !cur_add && s != 0;
-    const bool dbl = more && !next_add;
-    run([&](uint32_t t) {
-      if (t >= TW) {
-        if (sq) gtw_mul_prod<false>(F, F, S, t - TW);
-      } else if (more) {
-        if (next_add)
-          gtw_add_step_lane(TB, QA, nxt, xP, yP, t);
-        else
-          gtw_dbl_p1(TB, S2, t);
+    if (f_on) {
+      if (f_ph == 2) lines_used = fs + 1;
+      if (f_ph == 3) {
+        fs++;
+        fp_ = 0;
+      } else {
+        fp_++;
       }
-    });
-    run([&](uint32_t t) {
-      if (t >= TW) {
-        if (sq) gtw_mul_rec<false>(F, S, t - TW);
-      } else if (dbl) {
-        gtw_dbl_p2(TB, nxt, S2, t);
-      }
-    });
-    run([&](uint32_t t) {
-      if (t >= TW)
-        gtw_mul_prod<true>(F, cur, S, t - TW);
-      else if (dbl)
-        gtw_dbl_p3(TB, S2, xP, yP, t);
-    });
-    run([&](uint32_t t) {
-      if (t >= TW)
-        gtw_mul_rec<true>(F, S, t - TW);
-      else if (dbl)
-        gtw_dbl_p4(TB, nxt, S2, t);
-    });
-    cur_add = next_add;
+    }
   }
   run([&](uint32_t t) {  // f = conj(f): negate the odd w-coefficients
     if (t < 12 && ((t >> 1) & 1)) lds_st(F, (int)t, fp_neg(lds_ld(F, (int)t)));
@@ -516,7 +645,7 @@ struct GtwLds {
   uint32_t W[5 * GTW_FP12];     // final-exponentiation temporaries
   uint32_t L[GTW_FP12];         // lines (two buffers)
   uint32_t L1[GTW_FP12];
-  uint32_t S2[14 * BLS_NL];     // the Miller loop's T-chain products
+  uint32_t S2[28 * BLS_NL];     // the Miller loop's T-chain products
   uint32_t TB[(6 + 14) * BLS_NL];  // T + doubling temporaries
   uint32_t QA[4 * BLS_NL];      // Q affine
   uint32_t flag;

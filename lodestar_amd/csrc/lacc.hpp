@@ -79,6 +79,29 @@ BLS_INL void lds_st(uint32_t* b, int q, const fp& v) {
   for (int l = 0; l < BLS_NL; l++) b[q * BLS_NL + l] = v.l[l];
 }
 
+// a += coef * b[slot] (coef in -9 .. 9, as repeated terms)
+BLS_INL void lacc_term(lacc& a, const uint32_t* b, int slot, int coef) {
+  const fp v = lds_ld(b, slot);
+  for (int k = 0; k < (coef < 0 ? -coef : coef); k++) {
+    if (coef > 0)
+      lacc_add(a, v);
+    else
+      lacc_sub(a, v);
+  }
+}
+// a += coef * (component c of a Karatsuba Fp2 product whose three products P0, P1, P2 sit at slots k .. k + 2):
+// c = 0: P0 - P1, c = 1: P2 - P0 - P1
+BLS_INL void lacc_kara(lacc& a, const uint32_t* b, int k, int c, int coef) {
+  if (c == 0) {
+    lacc_term(a, b, k, coef);
+    lacc_term(a, b, k + 1, -coef);
+  } else {
+    lacc_term(a, b, k + 2, coef);
+    lacc_term(a, b, k, -coef);
+    lacc_term(a, b, k + 1, -coef);
+  }
+}
+
 // (x0 + x1 u)^2 = (x0 + x1)(x0 - x1) + (2 x0) x1 u : operands of component `comp`'s single product.  x0, x1:
 // normalized limbs, values <= 4p; the operands are lazy (limbs < 2^30, values < 12p: fp_mul's contract)
 BLS_INL void sqr_operands(const fp& x0, const fp& x1, int comp, fp& X, fp& Y) {

@@ -512,8 +512,12 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // MSM slices of the groups' set ranges (S_g = sum r_i sig_i).  Runs up to 32k sets (an isolated block's or
   // gossip call's latency) take half slices: twice the bucket workgroups at half the chain, 16k isolated sig_msm
   // 3.55 -> 2.80 ms; merged runs keep full slices (fewer bucket sums to combine: 100-step C2 3.13M vs 3.01M).
-  constexpr uint32_t kMsmHalfSliceMaxSets = 32768;
-  const uint32_t slice_len = n <= kMsmHalfSliceMaxSets ? MSM_SLICE / 2 : MSM_SLICE;
+  // Small runs (<= 1024 sets) take 32-set slices: a bucket lane's chain of mixed additions is ~len / 8 plus its
+  // spread (128 sets: ~25 additions on the slowest lane, 1.26 ms), the window lanes add the few slices up.
+  constexpr uint32_t kMsmHalfSliceMaxSets = 32768, kMsmSmallSliceMaxSets = 1024;
+  const uint32_t slice_len = n <= kMsmSmallSliceMaxSets  ? 32
+                             : n <= kMsmHalfSliceMaxSets ? MSM_SLICE / 2
+                                                         : MSM_SLICE;
   std::vector<uint32_t> slices, range_slices{0};
   for (uint32_t g = 0; g < ng0; g++)
     add_slices(slices, range_slices, job_sets(group_jobs[g].first).first, job_sets(group_jobs[g].second - 1).second,

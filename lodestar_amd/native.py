@@ -81,7 +81,7 @@ STAGES = ["sig_decode", "hash_to_g2", "pk_aggregate", "pk_finish", "sig_msm", "m
           "group_reduce", "group_check"]
 # the kernels each stage's HIP-event interval covers (rocprof lists them separately; k_batch_inv runs in both the
 # hash and the pubkey stage)
-KERNEL_OF_STAGE = ["k_sig_decode", "k_hash_prep+k_batch_inv+k_hash_map+k_hash_clear+k_h_affine", "k_pk_aggregate",
+KERNEL_OF_STAGE = ["k_sig_decode", "k_hash_prep+k_batch_inv+k_hash_map+k_hash_clear+k_hash_clear_coop+k_h_affine", "k_pk_aggregate",
                    "k_pk_finish+k_batch_inv+k_pk_affine", "k_job_mask+k_msm_bucket+k_msm_window+k_msm_horner",
                    "k_miller_lines+k_miller_acc", "k_f_runs+k_f_pairs+k_f_gather", "k_group_sig_miller+k_group_check"]
 

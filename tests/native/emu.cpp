@@ -180,7 +180,7 @@ int emu_g2c_add(const uint8_t* p192, int p_inf, const uint8_t* q192, int q_inf, 
 // on lanes 64 .. 191), lanes run in turn within each phase
 void emu_gtw_miller(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) {
   static uint32_t F[GTW_FP12], QA[4 * BLS_NL], TB[20 * BLS_NL], L0[GTW_FP12], L1[GTW_FP12], S[108 * BLS_NL],
-      S2[14 * BLS_NL];
+      S2[28 * BLS_NL];
   const g1a P = load_g1(p96);
   const g2a Q = load_g2(q192);
   lds_st(QA, 0, Q.x.c0);
