@@ -89,9 +89,9 @@ static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
 void launch_batch_inv(const uint32_t* src, uint32_t src_stride, int w0, uint32_t* dst, uint32_t n, hipStream_t s) {
   if (!n) return;
-  // up to 2048 elements (small runs, latency first): one element per lane, the inversion without the prefix
-  // chains (~0.1 ms instead of ~0.2 ms on a 128-set call's message and pubkey branches)
-  const uint32_t lanes = n <= 2048 ? n : (n + INV_K - 1) / INV_K;
+  // up to 16k elements (one wave per SIMD at most; small and medium runs, latency first): one element per lane,
+  // the inversion without the prefix chains (~0.1 ms instead of ~0.2 ms on each branch of a call that inverts)
+  const uint32_t lanes = n <= 16384 ? n : (n + INV_K - 1) / INV_K;
   hipLaunchKernelGGL(k_batch_inv, grid_for(lanes), dim3(WAVE), 0, s, src, src_stride, w0, dst, n, lanes);
 }
 void launch_pk_affine(const PipelineBuffers& b, uint32_t n, hipStream_t s) {
