@@ -72,11 +72,22 @@ __global__ __launch_bounds__(WAVE) void k_sig_subgroup_coop(PipelineBuffers b, u
   }
 }
 
+// the speculative MSM's mask (runtime.cpp): the sets whose signature decoded
+__global__ __launch_bounds__(WAVE) void k_spec_mask(PipelineBuffers b, uint32_t n_sets, uint8_t* spec) {
+  const uint32_t i = blockIdx.x * WAVE + threadIdx.x;
+  if (i < n_sets) spec[i] = b.status[i] == BLS_OK ? 1 : 0;
+}
+
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
-void launch_sig_decode(const PipelineBuffers& b, uint32_t n, hipStream_t s, bool coop) {
+void launch_spec_mask(const PipelineBuffers& b, uint32_t n, uint8_t* spec, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_spec_mask, grid_for(n), dim3(WAVE), 0, s, b, n, spec);
+}
+
+void launch_sig_decode(const PipelineBuffers& b, uint32_t n, hipStream_t s, bool coop, hipEvent_t decoded) {
   if (!n) return;
   hipLaunchKernelGGL(k_sig_decode, grid_for(n), dim3(WAVE), 0, s, b, n, !coop);
+  if (decoded) (void)hipEventRecord(decoded, s);
   if (coop)
     hipLaunchKernelGGL(k_sig_subgroup_coop, dim3((n + SG_GROUPS - 1) / SG_GROUPS), dim3(WAVE),
                        BLSGPU_EXCLUSIVE_SMALL ? exclusive_cu_lds<k_sig_subgroup_coop>() : 0, s, b, n);

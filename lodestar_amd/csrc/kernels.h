@@ -85,7 +85,11 @@ struct PipelineBuffers {
 
 // coop: small runs -- the [|z|] chains (subgroup check, cofactor clearing) as cooperative 16-lane doublings
 // (g2_coop.hpp), for latency
-void launch_sig_decode(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s, bool coop = false);
+// (decoded: recorded after the decode, before the small-run subgroup checks)
+void launch_sig_decode(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s, bool coop = false,
+                       hipEvent_t decoded = nullptr);
+// spec[i] = the signature of set i decoded (the speculative MSM's include mask)
+void launch_spec_mask(const PipelineBuffers& b, uint32_t n_sets, uint8_t* spec, hipStream_t s);
 void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s, bool coop = false);  // over the unique messages
 void launch_pk_aggregate(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 void launch_pk_finish(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);

@@ -106,7 +106,7 @@ inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 // (Device::st) and are shared by its slots, so a device needs kStreams hardware queues whatever its slot count.
 struct Slot {
   hipEvent_t join_in = nullptr, join_msg = nullptr, join_pk = nullptr, join_mask = nullptr, join_gsm = nullptr,
-             done = nullptr;  // no timing
+             join_dec = nullptr, join_msm = nullptr, done = nullptr;  // no timing
   hipEvent_t ev[2 * (kStages + 2)] = {};  // profile: (start, end) per stage; pairs kStages, kStages + 1 = the
                                           // Miller lines, the groups' MillerLoop(-g1, S) (parts of stages 5, 7)
   // d_in / h_in: every per-call input packed into one arena (one H2D transfer); d_res / h_res: job errors +
@@ -625,7 +625,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
 
   // byte arrays: flags n | mflags nm | unit_ok n | status 3n | include n ; results: job_err nj | ok ng
   const size_t ob_flags = 0, ob_mflags = al256(n), ob_unit = al256(ob_mflags + nm), ob_status = al256(ob_unit + n),
-               ob_include = al256(ob_status + 3 * (size_t)stride), bytes_total = al256(ob_include + stride);
+               ob_include = al256(ob_status + 3 * (size_t)stride), ob_spec = al256(ob_include + stride),
+               bytes_total = al256(ob_spec + stride);
   sl.d_bytes.ensure(bytes_total);
   const uint32_t max_ranges = std::max<uint32_t>(std::max(ng0, nj), 1);
   const size_t o_ok = al256(nj), res_bytes = o_ok + max_ranges;
@@ -743,10 +744,29 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     launch_pk_affine(pb, n, sp);
     end(3, sp);
     HIPCHK(hipEventRecord(sl.join_pk, sp));
-    // signatures, then the batch equation
+    // signatures, then the batch equation.  A small run on an idle device starts its MSM speculatively right after
+    // the decode, on the other pair's (idle) message stream, over the sets that decoded (spec mask), while the
+    // subgroup checks, the pubkeys and the job mask finish: S then includes the sets the job mask drops later (a
+    // failed subgroup check or pubkey, a job's other sets).  That only changes the failure path: a group whose S
+    // holds a dropped set fails its equation (barring a negligible r_i coincidence; an infinity signature never
+    // enters, and a dropped valid signature is in G2, so its term e(-g1, r sig) != 1) and its jobs are re-checked one
+    // by one with exact masks (the fallback), while a clean group's S is exact.  Saves the MSM's ~1.5 ms on the
+    // signature branch of a 128-set call.
+    const bool spec = BLSGPU_STREAM_PAIRS && coop && sl.alone;
+    hipStream_t smsm = spec ? d.st[2 * (1 - par) + 1] : s;
+    PipelineBuffers pbm = pb;
+    if (spec) pbm.include = db + ob_spec;
     beg(0, s);
-    launch_sig_decode(pb, n, s, coop);
+    launch_sig_decode(pb, n, s, coop, spec ? sl.join_dec : nullptr);
     end(0, s);
+    const uint32_t* d_slices = reinterpret_cast<uint32_t*>(din + o_slices);
+    const uint32_t* d_rslices = reinterpret_cast<uint32_t*>(din + o_rslices);
+    if (spec) {
+      HIPCHK(hipStreamWaitEvent(smsm, sl.join_dec, 0));
+      launch_spec_mask(pb, n, pbm.include, smsm);
+      launch_sig_msm(pbm, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, smsm);
+      HIPCHK(hipEventRecord(sl.join_msm, smsm));
+    }
     HIPCHK(hipStreamWaitEvent(s, sl.join_pk, 0));
     beg(4, s);
     launch_job_mask(pb, s);
@@ -766,9 +786,10 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     launch_group_tree(pb, d_franges, ng0, d_ftree, n_fruns, d_ftree + 2 * (size_t)n_fruns, f_level_end, sl.d_F.p, sm);
     end(6, sm);
     HIPCHK(hipEventRecord(sl.join_msg, sm));
-    const uint32_t* d_slices = reinterpret_cast<uint32_t*>(din + o_slices);
-    const uint32_t* d_rslices = reinterpret_cast<uint32_t*>(din + o_rslices);
-    launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s);
+    if (spec)
+      HIPCHK(hipStreamWaitEvent(s, sl.join_msm, 0));
+    else
+      launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s);
     end(4, s);
     // MillerLoop(-g1, S_g) of every group now, while the message branch still runs
     beg(kStages + 1, s);
@@ -1436,7 +1457,7 @@ void free_slot(Device* d, Slot* s) {
   if (last) (void)hipStreamSynchronize(last);
   for (auto& e : s->ev)
     if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk, s->join_mask, s->join_gsm, s->done})
+  for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk, s->join_mask, s->join_gsm, s->join_dec, s->join_msm, s->done})
     if (e) (void)hipEventDestroy(e);
   delete s;
 }
@@ -1446,7 +1467,8 @@ void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet sh
   HIPCHK(hipSetDevice(d->id));
   try {
     s->set_stream(d->st[kSig]);
-    for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk, &s->join_mask, &s->join_gsm, &s->done})
+    for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk, &s->join_mask, &s->join_gsm, &s->join_dec, &s->join_msm,
+                          &s->done})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
   } catch (HipError&) {
