@@ -330,8 +330,9 @@ def pmc_traffic(kernel, n_sets):
     with open(PMC_FILE) as fh:
         table = json.load(fh)["kernels"]
     # a stage is several launches ("k_a+k_b+..."); k_batch_inv's figure is per launch of either of its two uses
-    parts = kernel.split("+")
-    if not all(p in table and "FETCH_B_per_item" in table[p] for p in parts):
+    # (kernels of the stage that the measured command never launched, e.g. the small-run forms, are absent)
+    parts = [p for p in kernel.split("+") if p in table and "FETCH_B_per_item" in table[p]]
+    if not parts:
         return None
     per_unit = sum((table[p]["FETCH_B_per_item"] + table[p]["WRITE_B_per_item"]) * PMC_ITEMS_PER_UNIT.get(p, 1.0)
                    for p in parts)
