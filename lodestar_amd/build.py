@@ -23,7 +23,10 @@ OBJ_DIR = os.path.join(PKG, "build")  # per-TU objects, kept so an edit rebuilds
 
 # Per-translation-unit defines of the product build.  BLSGPU_TU_DEFINES overrides it for experiments:
 # "k_miller.hip=BLS_INLINE_PRODUCTS=1+OTHER=2;k_hash.hip=..." ("" = none).
-TU_DEFINES = {}
+# k_sig.hip with its decode helpers inlined (BLS_INLINE_BIG: sig_decode_point, fp2_sqrt and the (p-3)/4 power in
+# the kernel, no nested call frames): k_sig_decode's private segment 1,296 -> 496 B/lane at the same throughput
+# (profiles/r03_sigbig_ab.txt)
+TU_DEFINES = {"k_sig.hip": ["BLS_INLINE_BIG=1"]}
 
 
 def tu_defines():
@@ -54,7 +57,8 @@ def _tu_deps(src):
 
 
 def _deps():
-    return _headers() + [os.path.join(CSRC, s) for s in SOURCES]
+    # (this file too: its per-TU defines change the objects)
+    return _headers() + [os.path.join(CSRC, s) for s in SOURCES] + [os.path.abspath(__file__)]
 
 
 def up_to_date():

@@ -354,7 +354,7 @@ __device__ __forceinline__ void g2c_add(uint32_t* g, uint32_t tg, bool on = true
 // handles the exceptional cases).  Every lane of the workgroup calls it (the barriers); R in the group's LDS on entry and exit;
 // a group with `on` false (no point) runs the phases on its own LDS and never calls loadP.
 template <class LoadP>
-__device__ void g2c_mul_zabs(uint32_t* g, uint32_t tg, bool on, LoadP loadP) {
+__device__ __forceinline__ void g2c_mul_zabs(uint32_t* g, uint32_t tg, bool on, LoadP loadP) {
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
     g2c_dbl(g, tg);

@@ -223,13 +223,13 @@ BLS_INL fp2* fp12_slot(fp12& f, int k) {
     default: return &f.c1.c2;
   }
 }
-__device__ fp12 gtw_to_reg(const uint32_t* A) {
+__device__ __forceinline__ fp12 gtw_to_reg(const uint32_t* A) {
   fp12 f;
 #pragma unroll
   for (int k = 0; k < 6; k++) *fp12_slot(f, k) = fp2_make(lds_ld(A, 2 * k), lds_ld(A, 2 * k + 1));
   return f;
 }
-__device__ void gtw_from_reg(uint32_t* A, fp12 f) {
+__device__ __forceinline__ void gtw_from_reg(uint32_t* A, fp12 f) {
 #pragma unroll
   for (int k = 0; k < 6; k++) {
     lds_st(A, 2 * k, fp12_slot(f, k)->c0);
@@ -255,7 +255,7 @@ __device__ void gtw_pow_z(uint32_t* Y, const uint32_t* X, uint32_t* S, uint32_t 
   gtw_conj(Y, Y, t);  // z < 0
 }
 
-__device__ void gtw_final_exp(uint32_t* F, uint32_t* W, uint32_t* S, uint32_t t) {
+__device__ __forceinline__ void gtw_final_exp(uint32_t* F, uint32_t* W, uint32_t* S, uint32_t t) {
   uint32_t *U = W, *V = W + GTW_FP12, *M = W + 2 * GTW_FP12, *T = W + 3 * GTW_FP12, *X = W + 4 * GTW_FP12;
   // f1 = conj(f) / f = conj(f)^2 / (f conj(f)), where f conj(f) = a0^2 - v a1^2 lies in Fp6: the two Fp12
   // products are cooperative and lane 0 inverts only an Fp6 (the lane-0 Fp12 inverse took 271 us in the probe)
