@@ -523,12 +523,14 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     add_slices(slices, range_slices, job_sets(group_jobs[g].first).first, job_sets(group_jobs[g].second - 1).second,
                slice_len);
   const uint32_t n_slices = (uint32_t)(slices.size() / 2);
-  // F_g = prod of the group's Miller chunks as a product tree (launch_group_tree): with more than 8192 chunks, runs
-  // of f_k consecutive chunks first (lane-serial: a 128-lane cooperative product costs ~6x the lane time), then
-  // pair levels of stride f_k, 2 f_k, ... (one cooperative workgroup per pair); ftree = runs, then the pairs
+  // F_g = prod of the group's Miller chunks as a product tree (launch_group_tree): with more than 16384 chunks (merged
+  // runs), runs of f_k consecutive chunks first (lane-serial: a 128-lane cooperative product costs ~6x the lane
+  // time) down to <= 8192 heads, then pair levels of stride f_k, 2 f_k, ... (one cooperative workgroup per pair);
+  // ftree = runs, then the pairs.  Up to 16384 chunks (a 16k call) the tree starts at the chunks: its latency.
   std::vector<uint32_t> ftree, f_level_end;
   uint32_t f_k = 1, f_max = 0;
-  while (n_chunks / f_k > 8192 && f_k < 16) f_k *= 2;
+  if (n_chunks > 16384)
+    while (n_chunks / f_k > 8192 && f_k < 16) f_k *= 2;
   for (uint32_t g = 0; g < ng0; g++) f_max = std::max(f_max, g_chunks[2 * g + 1] - g_chunks[2 * g]);
   if (f_k > 1)
     for (uint32_t g = 0; g < ng0; g++)

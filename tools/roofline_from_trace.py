@@ -25,19 +25,22 @@ def main(trace, bench_json, out=None):
             continue
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         if s >= t0 and e <= t1:
-            ev.append((s, e, n, int(r["Grid_Size_X"])))
+            ev.append((s, e, n, int(r["Grid_Size_X"]), r.get("Queue_Id", "0")))
     ev.sort()
-    # a run's stage starts at its k_hash_prep (names[0]) and ends at the next run's first kernel
-    runs, cur = [], None
-    for s, e, n, g in ev:
+    # a run's stage starts at its k_hash_prep (names[0]) and holds the stage kernels that follow it on the same
+    # queue up to that queue's next k_hash_prep (consecutive runs alternate between stream pairs and overlap in
+    # time, so grouping by time alone would hand one run's tail to the next)
+    runs, cur = [], {}
+    for s, e, n, g, q in ev:
         if n == names[0]:
-            cur = {"start": s, "end": e, "kernel_ns": 0, "kernels": 0, "prep_grid": g}
-            runs.append(cur)
-        if cur is None:
+            cur[q] = {"start": s, "end": e, "kernel_ns": 0, "kernels": 0, "prep_grid": g}
+            runs.append(cur[q])
+        if q not in cur:
             continue
-        cur["end"] = max(cur["end"], e)
-        cur["kernel_ns"] += e - s
-        cur["kernels"] += 1
+        c = cur[q]
+        c["end"] = max(c["end"], e)
+        c["kernel_ns"] += e - s
+        c["kernels"] += 1
     # only runs whose last kernel (names[-1]) landed inside the window
     done = [r for r in runs if r["kernels"] >= len(names)]
     span = sum(r["end"] - r["start"] for r in done) / len(done) / 1e6
