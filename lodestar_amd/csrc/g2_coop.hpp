@@ -290,9 +290,17 @@ BLS_INL g2j g2c_ld_q(const uint32_t* g) { return g2c_ld_point(g + (G2C_Q - G2C_R
 BLS_INL void g2c_st_q(uint32_t* g, const g2j& q) { g2c_st_point(g + (G2C_Q - G2C_R) * BLS_NL, q); }
 // writer lane tg < 6 of R5: reads g, writes w (the same buffer on the device: the lanes of a group share a wave
 // and all read before any writes; the host model writes a copy)
+// the exceptional cases' lane-serial addition, out of line: inlined, jac_add's temporaries would raise the register
+// pressure of every chain loop that adds (the subgroup check's loop spilled ~200 scratch accesses)
+#if defined(__HIPCC__)
+__device__ __noinline__
+#else
+static
+#endif
+void g2c_add_exc(const uint32_t* g, uint32_t* w) { g2c_st_point(w, jac_add(g2c_ld_point(g), g2c_ld_q(g))); }
 BLS_INL void g2c_add_r5(const uint32_t* g, uint32_t* w, uint32_t tg, bool exc) {
   if (exc) {
-    if (tg == 0) g2c_st_point(w, jac_add(g2c_ld_point(g), g2c_ld_q(g)));
+    if (tg == 0) g2c_add_exc(g, w);
     return;
   }
   fp v;
