@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define BLSGPU_ABI_VERSION 4
+#define BLSGPU_ABI_VERSION 5
 
 enum blsgpu_code {
   BLSGPU_OK = 0,
@@ -53,7 +53,9 @@ enum blsgpu_code {
   BLSGPU_DEVICE_ERROR = 11,      /* HIP failure: every job of the call is rejected, never `false` */
   BLSGPU_ERR_ARGS = 100,         /* call-level: malformed arguments */
   BLSGPU_ERR_NO_DEVICE = 101,    /* call-level: no usable MI355X */
-  BLSGPU_ERR_CLOSED = 102        /* call-level: context destroyed (QUEUE_ERROR_QUEUE_ABORTED) */
+  BLSGPU_ERR_CLOSED = 102,       /* call-level: context destroyed (QUEUE_ERROR_QUEUE_ABORTED) */
+  BLSGPU_ERR_ENTROPY = 103       /* call-level: seed 0 and the OS gave no randomness for the batch scalars: the call
+                                    is refused (every job -BLSGPU_DEVICE_ERROR), never run with guessable scalars */
 };
 
 typedef struct blsgpu_ctx blsgpu_ctx;
@@ -84,7 +86,9 @@ typedef struct blsgpu_batch {
   const uint8_t* sigs;     /* [sig_stride * n_sets] untrusted signature bytes */
   const uint32_t* sig_len; /* [n_sets]: 96 (compressed) or 192 (uncompressed); else BLST_INVALID_SIZE */
   uint32_t sig_stride;
-  uint64_t seed; /* random-linear-combination scalars: fixed seed for comparison runs, 0 = OS CSPRNG */
+  uint64_t seed; /* random-linear-combination scalars (ChaCha20 keystream, one 64-bit word per set): 0 = a fresh
+                  * 256-bit key from getrandom per call (production; BLSGPU_ERR_ENTROPY if unavailable), else a key
+                  * derived from this seed (deterministic comparison runs only) */
 } blsgpu_batch;
 /* Identical signing roots within a call are hashed to G2 once, and within a batch group the sets that sign
  * the same root are paired once, against sum_i r_i pk_i (option "dedupe", default 1). */
@@ -121,9 +125,10 @@ int blsgpu_device_count(const blsgpu_ctx* ctx);
 
 /* Trusted pubkey table (replicated on every device): entries [first_index, first_index + n) from
  * 96-byte uncompressed affine encodings.  Returns BLSGPU_BAD_ENCODING / _POINT_NOT_ON_CURVE for a
- * malformed entry (nothing is written on that device in that case), BLSGPU_ERR_ARGS when first_index is
- * beyond the current table size (no gaps).  Devices are updated one after the other; a call that uses the
- * new indices before the upload returns may fail with BLSGPU_ERR_ARGS, never verify against stale keys. */
+ * malformed entry (nothing is written in that case), BLSGPU_ERR_ARGS when first_index is beyond the current
+ * table size (no gaps).  The devices decode and store their replicas concurrently (one host thread each); each
+ * device's table grows under its own lock, so a call that uses the new indices before the upload returns may fail
+ * with BLSGPU_ERR_ARGS on a device not yet updated, never verify against stale keys. */
 int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* pk96, uint32_t n);
 uint32_t blsgpu_pubkeys_count(const blsgpu_ctx* ctx);
 
@@ -139,7 +144,7 @@ typedef void (*blsgpu_done_cb)(void* user, int status);
 int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result, blsgpu_stats* stats,
                   blsgpu_done_cb done, void* user);
 
-/* Tunables: "group_sets" (sets per batch group before a new one opens, default 1024), "slots" (runtime slots
+/* Tunables ("slots" may not be changed from a done callback: BLSGPU_ERR_ARGS): "group_sets" (sets per batch group before a new one opens, default 1024), "slots" (runtime slots
  * per device, 1..64; default by hardware queues), "max_devices" (devices one call may shard over, default all),
  * "dedupe" (message dedupe + same-message pairing, 0/1, default 1), "miller_k" (pairings per Miller
  * accumulator sharing its Fp12 squarings, 1..64; default 0 = by run size: 1 below 131072 pairings, 2 below
@@ -193,6 +198,21 @@ int blsgpu_signing_roots(blsgpu_ctx* ctx, int kind, uint32_t n, const uint8_t* o
 int blsgpu_shard_jobs(const uint32_t* job_first_set, const uint32_t* set_pk_first, uint32_t n_jobs,
                       uint32_t n_parts, uint32_t* part_first_job);
 
+/* The batch scalar words blsgpu_verify would use for `b` (only n_sets, n_jobs, job_first_set, job_flags and seed
+ * are read): words[i] for set i, 0 = r = 1 (a single-set non-batchable job: CoreVerify).  With seed 0 every call
+ * draws a fresh key, so two calls differ.  Returns BLSGPU_ERR_ENTROPY when seed is 0 and the OS gives no
+ * randomness.  Pure host code. */
+int blsgpu_batch_scalars(const blsgpu_batch* b, uint64_t* words);
+
+/* Test hook: fault injection, process-wide.  After `skip` more events, the next `count` events fail:
+ *   BLSGPU_INJECT_ENTROPY: an entropy draw (seed-0 calls, blsgpu_batch_scalars) -> BLSGPU_ERR_ENTROPY;
+ *   BLSGPU_INJECT_DEVICE: a pipeline run, once its batch pass completed, as if a HIP call had failed -> every job
+ *     of every call in that run -BLSGPU_DEVICE_ERROR (never 0); the dispatcher keeps serving later calls.
+ * count 0 disarms. */
+#define BLSGPU_INJECT_ENTROPY 1
+#define BLSGPU_INJECT_DEVICE 2
+int blsgpu_debug_inject(int what, int64_t skip, int64_t count);
+
 /* "BLST_INVALID_SIZE", ... for job codes; NULL for unknown codes. */
 const char* blsgpu_code_name(int code);
 
@@ -201,7 +221,8 @@ const char* blsgpu_code_name(int code);
  *     3 miller(96,192->576) 4 final_exp(576->576) 5 g1_mul_u64(96,8->96) 6 g2_mul_u64(192,8->192)
  *     7 sign(sk32||msg32 -> 96 compressed) 8 sk_to_pk(sk32 -> 96 uncompressed)   (workload generation)
  *     9 g2_mul_scalar_word(192,8 -> 192; out_stride >= 2880) 10 g1_mul_scalar_word(96,8 -> 96; >= 1440):
- *       the batch scalar r = 2w + 1 - 2^64 of a scalar word w (regular signed window)
+ *       the batch scalar r = a + b*lambda of a scalar word w (a = 2 lo + 1 - 2^32, b = 2 hi + 1 - 2^32 from w's
+ *       32-bit halves, lambda = -z^2), word 0 = r = 1
  * Returns BLSGPU_OK or an error. */
 int blsgpu_debug_op(blsgpu_ctx* ctx, int op, uint32_t n, const uint8_t* in, uint32_t in_stride,
                     uint8_t* out, uint32_t out_stride, int32_t* status);

@@ -52,7 +52,8 @@ def _tu_deps(src):
     """runtime.cpp sees only the C-ABI header and the kernel launch declarations; a kernel TU sees every
     arithmetic header."""
     if src.endswith(".cpp"):
-        return [os.path.join(CSRC, src), os.path.join(CSRC, "kernels.h"), os.path.join(ROOT, "include", "blsgpu.h")]
+        return [os.path.join(CSRC, src), os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "batch_rand.hpp"),
+                os.path.join(ROOT, "include", "blsgpu.h")]
     return [os.path.join(CSRC, src)] + _headers()
 
 

@@ -2,6 +2,8 @@
 // base[w * stride + i], so the 64 lanes of a wave touch 64 consecutive words per limb -- coalesced) and
 // the small scalar-multiplication loops.  Included by every k_*.hip translation unit.
 #pragma once
+#include <atomic>
+
 #include "kernels.h"
 #include "ops.hpp"
 
@@ -246,13 +248,19 @@ __device__ jac<F> jac_mul_words(const jac<F>& P, const uint32_t* k, int nw) {
 // a 128-set call's trace).  Launched with this much extra dynamic LDS, one such workgroup fills the CU's LDS (160 KB on
 // gfx950) beyond what any other kernel of the pipeline needs (<= 36 KB), so the CU runs it alone.  0 when the device
 // does not allow it (the launch then simply shares CUs).
-// (One cached value per kernel: the template parameter is the kernel itself -- keyed by its type, kernels of one
-// signature shared the first one's padding, and a larger kernel's static LDS plus that padding overflowed the CU.)
+// (One cached value per kernel and device: the template parameter is the kernel itself -- keyed by its type, kernels
+// of one signature shared the first one's padding, and a larger kernel's static LDS plus that padding overflowed the
+// CU -- and hipFuncSetAttribute applies to the current device only, so each device computes and sets its own.)
 template <auto kernel>
 inline size_t exclusive_cu_lds() {
-  static const size_t pad = [&]() -> size_t {
-    int dev = 0, max_block = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
+  constexpr int kMaxDev = 64;
+  static std::atomic<int64_t> cache[kMaxDev];  // zero-initialized: 0 = not yet computed, else pad + 1
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
+  const int64_t c = cache[dev].load(std::memory_order_acquire);
+  if (c) return (size_t)(c - 1);
+  const size_t pad = [&]() -> size_t {
+    int max_block = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&max_block, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&per_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess)
       return 0;
@@ -267,5 +275,6 @@ inline size_t exclusive_cu_lds() {
       return 0;
     return pad_b;
   }();
+  cache[dev].store((int64_t)pad + 1, std::memory_order_release);
   return pad;
 }

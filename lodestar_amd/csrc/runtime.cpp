@@ -32,10 +32,12 @@
 #include <mutex>
 #include <shared_mutex>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
 #include "../../include/blsgpu.h"
+#include "batch_rand.hpp"
 #include "kernels.h"
 
 namespace {
@@ -177,14 +179,11 @@ struct Device {
   std::atomic<uint32_t> run_seq{0};  // run counter: the stream pair of a run (BLSGPU_STREAM_PAIRS)
 };
 
-inline uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
-  // i-th output of the SplitMix64 stream seeded with `seed` (counter form: state_i = seed + (i+1) gamma)
-  uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z = z ^ (z >> 31);
-  return z ? z : 1;
-}
+// Device-failure injection (blsgpu_debug_inject, tests only): the next `count` pipeline runs after `skip` more fail as
+// if a HIP call had failed once their batch pass completed.
+std::atomic<int64_t> g_fail_run_skip{0}, g_fail_run_count{0};
+// set on the runtime's dispatcher threads (a "slots" change from a done callback would join its own thread)
+thread_local bool tl_dispatcher = false;
 
 struct Options {  // snapshot taken at the start of each call
   int64_t group_sets = 1024;
@@ -267,7 +266,8 @@ struct Call {
   Owned* owned = nullptr;
   int8_t* job_result = nullptr;
   blsgpu_stats* stats = nullptr;
-  uint64_t seed = 0;
+  uint64_t seed = 0;       // message-index hash key (comparison runs: the batch seed)
+  batch_rand::Key key{};   // batch scalars: ChaCha20 keystream under this key (batch_rand.hpp)
   uint32_t max_index = 0;  // largest pubkey-table index of the call (table mode)
   Options opt;
   std::vector<Shard> shards;
@@ -381,8 +381,10 @@ void release_inflight(Device& d, Slot& sl) {
 // With `plan` (group_policy 1), the groups are the plan's job ranges instead of >= group_sets packing, and the
 // batchRetries / batchSigsSuccess metrics count the plan's batchable chunks the way the worker does (worker.ts:
 // 56-84: a chunk that throws or returns false is one retry; a chunk that verifies adds all its sets).
+// scal_words: the shard's batch scalar words (shard_scalars' rule, in the batch's set order); seed: the message
+// index's hash key.
 int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_t* job_result, uint64_t seed,
-              const Options& opt, uint32_t max_index, blsgpu_stats& st, const uint64_t* scal_words = nullptr,
+              const Options& opt, uint32_t max_index, blsgpu_stats& st, const uint64_t* scal_words,
               const std::vector<GroupPlanEntry>* plan = nullptr) {
   const uint32_t n = sh.set_end - sh.set_begin;
   const uint32_t nj = sh.job_end - sh.job_begin;
@@ -411,7 +413,6 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       group_jobs.push_back({g.first, g.end});
       group_batchable.push_back(g.batchable);
     }
-    // scalars come from scal_words (the caller applies shard_scalars' rule in the calls' own set order)
   } else {
     uint32_t cur_sets = 0;
     bool open = false;
@@ -425,12 +426,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       }
       if (!batchable) {
         group_jobs.push_back({j, j + 1});
-        // single-set non-batchable job: CoreVerify (r = 1, scalar word 0); multi-set: random linear combination
-        for (uint32_t i = a; i < e; i++) scal[i] = (e - a == 1) ? 0ull : splitmix64_at(seed, s0 + i);
         open = false;
         continue;
       }
-      for (uint32_t i = a; i < e; i++) scal[i] = splitmix64_at(seed, s0 + i);
       if (!open || cur_sets >= (uint32_t)opt.group_sets) {
         group_jobs.push_back({j, j});
         cur_sets = 0;
@@ -440,7 +438,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       cur_sets += e - a;
     }
   }
-  if (scal_words) memcpy(scal.data(), scal_words, (size_t)n * 8);  // merged calls: each part's own seed
+  // scalars: the caller applies shard_scalars' rule (each merged call its own key, in the calls' own set order)
+  memcpy(scal.data(), scal_words, (size_t)n * 8);
   auto job_sets = [&](uint32_t j) {
     const uint32_t gj = sh.job_begin + j;
     return std::make_pair(b.job_first_set[gj] - s0, b.job_first_set[gj + 1] - s0);
@@ -711,6 +710,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // short next to the message branch; see sp below for small runs) and consecutive runs use the other pair; without,
   // each branch has its own stream shared by every run.
   const bool prof = opt.profile;
+  const bool spec = BLSGPU_STREAM_PAIRS && coop && sl.alone;  // speculative MSM (below)
   // A small run that found the device idle puts its pubkey branch on the other pair's (idle) signature stream, beside
   // its own signature decode and subgroup checks instead of in front of them: the signature branch was a small
   // call's critical path (C1 serial trace: 7.25 ms vs the message branch's 6.15).
@@ -754,7 +754,6 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     // enters, and a dropped valid signature is in G2, so its term e(-g1, r sig) != 1) and its jobs are re-checked one
     // by one with exact masks (the fallback), while a clean group's S is exact.  Saves the MSM's ~1.5 ms on the
     // signature branch of a 128-set call.
-    const bool spec = BLSGPU_STREAM_PAIRS && coop && sl.alone;
     hipStream_t smsm = spec ? d.st[2 * (1 - par) + 1] : s;
     PipelineBuffers pbm = pb;
     if (spec) pbm.include = db + ob_spec;
@@ -808,6 +807,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     HIPCHK(hipEventRecord(sl.done, stl));
   }
   HIPCHK(hipEventSynchronize(sl.done));
+  if (batch_rand::take_injection(g_fail_run_skip, g_fail_run_count)) throw HipError{hipErrorLaunchFailure};
   release_inflight(d, sl);
   st.groups += ng0;
   st.unique_messages += n_umsg;
@@ -837,8 +837,23 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   std::vector<uint32_t> retry;  // clean jobs of failed groups, each re-checked on its own
   for (uint32_t g = 0; g < ng0; g++) {
     std::vector<uint32_t> clean;
-    for (uint32_t j = group_jobs[g].first; j < group_jobs[g].second; j++)
-      if (jr[j] == 2) clean.push_back(j);
+    bool dropped = false;  // a rejected job of the group has sets (they may sit in a speculative S_g)
+    for (uint32_t j = group_jobs[g].first; j < group_jobs[g].second; j++) {
+      if (jr[j] == 2)
+        clean.push_back(j);
+      else if (job_sets(j).second > job_sets(j).first)
+        dropped = true;
+    }
+    // Speculative MSM (spec): S_g summed every decoded set of the group, so a group with a rejected job is not the
+    // equation of its clean jobs -- its verdict (pass or fail) is not read; every clean job is re-checked on its own
+    // with exact masks (the fallback's own S_j, F_j).  Only the failure path pays.  The subgroup check's writes to
+    // sig_aff, unordered with the speculative MSM's reads, can likewise only reach such a group.
+    if (spec && dropped && !clean.empty()) {
+      if (plan && group_batchable[g]) st.batch_retries++;
+      if (!plan && clean.size() > 1) st.batch_retries++;
+      retry.insert(retry.end(), clean.begin(), clean.end());
+      continue;
+    }
     if (plan) {  // the worker's metrics: a chunk with a throwing job or a failed equation is one retry
       if (!group_batchable[g]) {
       } else if (clean.size() == group_jobs[g].second - group_jobs[g].first && sl.h_res.p[o_ok + g]) {
@@ -1071,14 +1086,14 @@ void finish_call(Call* c) {
 // pubkey mode of a batch: 0 table, 1 one key per set (bytes), 2 bytes aggregate
 inline int pk_mode(const blsgpu_batch& b) { return !b.pk_bytes ? 0 : (b.set_pk_first ? 2 : 1); }
 
-// Batch scalar words of a shard (shard-relative), the rule run_shard applies: single-set non-batchable jobs
-// use r = 1 (word 0, CoreVerify), every other set a SplitMix64 word of the call's seed.
-void shard_scalars(const blsgpu_batch& b, const Shard& sh, uint64_t seed, uint64_t* out) {
+// Batch scalar words of a shard (shard-relative): single-set non-batchable jobs use r = 1 (word 0, CoreVerify,
+// maybeBatch.ts:34-38), every other set i the call's keystream word i (batch_rand.hpp).
+void shard_scalars(const blsgpu_batch& b, const Shard& sh, const batch_rand::Key& key, uint64_t* out) {
+  if (sh.set_end > sh.set_begin) batch_rand::words(key, sh.set_begin, sh.set_end - sh.set_begin, out);
   for (uint32_t j = sh.job_begin; j < sh.job_end; j++) {
     const uint32_t a = b.job_first_set[j], e = b.job_first_set[j + 1];
     const bool batchable = b.job_flags && (b.job_flags[j] & 1u);
-    for (uint32_t i = a; i < e; i++)
-      out[i - sh.set_begin] = (!batchable && e - a == 1) ? 0ull : splitmix64_at(seed, i);
+    if (!batchable && e - a == 1) out[a - sh.set_begin] = 0;
   }
 }
 
@@ -1093,10 +1108,7 @@ int run_pool_policy(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh,
                     const Options& opt, uint32_t max_index, blsgpu_stats& st, const uint64_t* scal_words) {
   const uint32_t s0 = sh.set_begin, n = sh.set_end - sh.set_begin;
   std::vector<uint64_t> scal0(std::max<uint32_t>(n, 1));
-  if (scal_words)
-    memcpy(scal0.data(), scal_words, (size_t)n * 8);
-  else
-    shard_scalars(b, sh, seed, scal0.data());
+  memcpy(scal0.data(), scal_words, (size_t)n * 8);
   struct Sub {
     uint32_t call, a, e;
     bool batchable;
@@ -1202,7 +1214,7 @@ int run_pool_policy(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh,
 
 // One shard of a call (or a merged batch) under the call's group policy.
 int run_call_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_t* job_result, uint64_t seed,
-                   const Options& opt, uint32_t max_index, blsgpu_stats& st, const uint64_t* scal_words = nullptr) {
+                   const Options& opt, uint32_t max_index, blsgpu_stats& st, const uint64_t* scal_words) {
   if (opt.group_policy == 1) return run_pool_policy(d, sl, b, sh, job_result, seed, opt, max_index, st, scal_words);
   return run_shard(d, sl, b, sh, job_result, seed, opt, max_index, st, scal_words);
 }
@@ -1266,7 +1278,7 @@ void run_merged(Device& d, Slot& sl, const std::vector<Task>& parts, std::vector
       const Task& t = parts[p];
       const Shard& sh = t.call->shards[t.shard];
       const blsgpu_batch& b = t.call->b;
-      shard_scalars(b, sh, t.call->seed, scal.data() + so);
+      shard_scalars(b, sh, t.call->key, scal.data() + so);
       for (uint32_t j = sh.job_begin; j < sh.job_end; j++) {
         jfs.push_back(so + b.job_first_set[j + 1] - sh.set_begin);
         flags.push_back(b.job_flags ? b.job_flags[j] : 0);
@@ -1345,7 +1357,10 @@ void run_task(Device& d, Slot& sl, const Task& t) {
       if (!table_covers(d, c, sh)) {
         rc = BLSGPU_ERR_ARGS;
       } else {
-        rc = run_call_shard(d, sl, c->b, sh, c->job_result, c->seed, c->opt, c->max_index, c->sst[t.shard]);
+        std::vector<uint64_t> scal(std::max<uint32_t>(sh.set_end - sh.set_begin, 1));
+        shard_scalars(c->b, sh, c->key, scal.data());
+        rc = run_call_shard(d, sl, c->b, sh, c->job_result, c->seed, c->opt, c->max_index, c->sst[t.shard],
+                            scal.data());
         c->sst[t.shard].run_calls = 1;
       }
     } catch (...) {
@@ -1367,6 +1382,7 @@ inline uint32_t task_sets(const Task& t) {
 // (up to merge_sets sets), runs them, completes their calls.  Exits when the device stops (queue drained) or when
 // the slot is retired (option "slots" lowered).
 void worker_loop(Device* d, Slot* sl) {
+  tl_dispatcher = true;
   (void)hipSetDevice(d->id);
   for (;;) {
     std::vector<Task> parts;
@@ -1499,8 +1515,16 @@ void resize_slots(Device* d, int64_t want) {
     }
   }
   d->q_cv.notify_all();
-  for (auto& t : joins) t.join();
-  for (Slot* s : gone) free_slot(d, s);
+  // (set_option refuses "slots" on a dispatcher thread, so no thread joins itself here; a failing join leaves the
+  // retired dispatcher to finish on its own and keeps its slot: detached, never destroyed while joinable)
+  for (size_t k = 0; k < joins.size(); k++) {
+    try {
+      joins[k].join();
+      free_slot(d, gone[k]);
+    } catch (std::system_error&) {
+      joins[k].detach();
+    }
+  }
 }
 
 void destroy_device(Device* d) {
@@ -1570,11 +1594,22 @@ void launch_call(blsgpu_ctx* ctx, Call* c) {
   }
 }
 
-uint64_t resolve_seed(uint64_t seed) {
-  while (seed == 0) {
-    if (getrandom(&seed, sizeof(seed), 0) != (ssize_t)sizeof(seed)) seed = 0x4C4F444553544152ull;
+// The call's scalar key and message-index hash key from its seed (batch_rand.hpp): seed 0 = 256 bits of OS
+// entropy, else the comparison-run key of the seed.  false = no entropy: the call must fail (never a constant).
+bool resolve_key(uint64_t seed, batch_rand::Key& key, uint64_t& hash_key) {
+  if (seed == 0) {
+    if (!batch_rand::os_key(key)) return false;
+    hash_key = (uint64_t)key.k[6] | ((uint64_t)key.k[7] << 32);
+  } else {
+    key = batch_rand::seed_key(seed);
+    hash_key = seed;
   }
-  return seed;
+  return true;
+}
+
+void reject_all(const blsgpu_batch* b, int8_t* job_result, int code) {
+  if (job_result)
+    for (uint32_t j = 0; j < b->n_jobs; j++) job_result[j] = (int8_t)-code;
 }
 
 Options snapshot(blsgpu_ctx* ctx) {
@@ -1730,7 +1765,8 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return BLSGPU_ERR_ARGS;
   std::string k(key);
   if (k == "slots") {
-    if (value < 1 || value > 64) return BLSGPU_ERR_ARGS;
+    // not from a dispatcher thread (a done callback): retiring its own slot would join itself
+    if (value < 1 || value > 64 || tl_dispatcher) return BLSGPU_ERR_ARGS;
     std::lock_guard<std::mutex> sk(ctx->slots_mu);
     ctx->slots_per_device = value;
     if (ctx->slots_started) {
@@ -1838,7 +1874,11 @@ int blsgpu_verify(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, bl
   c.b = *b;
   c.job_result = job_result;
   c.stats = stats;
-  c.seed = resolve_seed(b->seed);
+  if (!resolve_key(b->seed, c.key, c.seed)) {
+    reject_all(b, job_result, BLSGPU_DEVICE_ERROR);
+    leave(ctx);
+    return BLSGPU_ERR_ENTROPY;
+  }
   c.max_index = max_table_index(b);
   c.opt = snapshot(ctx);
   c.sync = true;
@@ -1864,8 +1904,17 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, bl
   if (v) return v;
   if (b->n_jobs && !job_result) return BLSGPU_ERR_ARGS;
   if (!enter(ctx)) return BLSGPU_ERR_CLOSED;
+  batch_rand::Key key;
+  uint64_t hash_key = 0;
+  if (!resolve_key(b->seed, key, hash_key)) {
+    reject_all(b, job_result, BLSGPU_DEVICE_ERROR);
+    leave(ctx);
+    return BLSGPU_ERR_ENTROPY;
+  }
   // deep-copy the inputs so the caller may reuse its buffers immediately
   Call* c = new Call();
+  c->key = key;
+  c->seed = hash_key;
   Owned* o = new Owned();
   c->ctx = ctx;
   c->owned = o;
@@ -1896,7 +1945,6 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, bl
   }
   c->job_result = job_result;
   c->stats = stats;
-  c->seed = resolve_seed(b->seed);
   c->max_index = max_table_index(&c->b);
   c->opt = snapshot(ctx);
   c->done = done;
@@ -1913,6 +1961,32 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, bl
     return e;
   }
   launch_call(ctx, c);
+  return BLSGPU_OK;
+}
+
+int blsgpu_batch_scalars(const blsgpu_batch* b, uint64_t* words) {
+  if (!b || !b->job_first_set || (b->n_sets && !words)) return BLSGPU_ERR_ARGS;
+  if (b->n_jobs && b->job_first_set[b->n_jobs] != b->n_sets) return BLSGPU_ERR_ARGS;
+  batch_rand::Key key;
+  uint64_t hash_key = 0;
+  if (!resolve_key(b->seed, key, hash_key)) return BLSGPU_ERR_ENTROPY;
+  shard_scalars(*b, Shard{0, b->n_jobs, 0, b->n_sets}, key, words);
+  return BLSGPU_OK;
+}
+
+int blsgpu_debug_inject(int what, int64_t skip, int64_t count) {
+  if (skip < 0 || count < 0) return BLSGPU_ERR_ARGS;
+  if (what == BLSGPU_INJECT_ENTROPY) {
+    batch_rand::inject_count() = 0;
+    batch_rand::inject_skip() = skip;
+    batch_rand::inject_count() = count;
+  } else if (what == BLSGPU_INJECT_DEVICE) {
+    g_fail_run_count = 0;
+    g_fail_run_skip = skip;
+    g_fail_run_count = count;
+  } else {
+    return BLSGPU_ERR_ARGS;
+  }
   return BLSGPU_OK;
 }
 
@@ -1940,6 +2014,7 @@ const char* blsgpu_code_name(int code) {
     case BLSGPU_ERR_ARGS: return "BLSGPU_ERR_ARGS";
     case BLSGPU_ERR_NO_DEVICE: return "BLSGPU_ERR_NO_DEVICE";
     case BLSGPU_ERR_CLOSED: return "QUEUE_ERROR_QUEUE_ABORTED";
+    case BLSGPU_ERR_ENTROPY: return "BLSGPU_ERR_ENTROPY";
     default: return nullptr;
   }
 }

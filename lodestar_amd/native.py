@@ -21,6 +21,10 @@ DEVICE_ERROR = 11
 ERR_ARGS = 100
 ERR_NO_DEVICE = 101
 ERR_CLOSED = 102
+ERR_ENTROPY = 103
+# blsgpu_debug_inject targets
+INJECT_ENTROPY = 1
+INJECT_DEVICE = 2
 
 EXPORTED_SYMBOLS = [
     "blsgpu_init",
@@ -39,6 +43,8 @@ EXPORTED_SYMBOLS = [
     "blsgpu_shard_jobs",
     "blsgpu_get_option",
     "blsgpu_chunkify",
+    "blsgpu_batch_scalars",
+    "blsgpu_debug_inject",
 ]
 ROOT_OBJECT = 0
 ROOT_ATTESTATION_DATA = 1
@@ -130,6 +136,10 @@ def load():
     lib.blsgpu_shard_jobs.argtypes = [vp, vp, u32, u32, vp]
     lib.blsgpu_get_option.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
     lib.blsgpu_chunkify.argtypes = [u32, u32, vp, vp]
+    lib.blsgpu_batch_scalars.argtypes = [ctypes.POINTER(Batch), vp]
+    lib.blsgpu_batch_scalars.restype = ctypes.c_int
+    lib.blsgpu_debug_inject.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
+    lib.blsgpu_debug_inject.restype = ctypes.c_int
     _lib = lib
     return lib
 
@@ -160,6 +170,36 @@ def chunkify(length, min_per_chunk):
     if rc != OK:
         raise ValueError(f"blsgpu_chunkify -> {code_name(rc)}")
     return [list(range(int(out[k]), int(out[k + 1]))) for k in range(nc.value)]
+
+
+def batch_scalars(job_first_set, job_flags=None, seed=0):
+    """The batch scalar words a call would use (C-ABI blsgpu_batch_scalars, pure host code): uint64 array, one word
+    per set (0 = r = 1).  Raises RuntimeError(ERR_ENTROPY) when seed is 0 and the OS gives no randomness."""
+    jfs = np.ascontiguousarray(job_first_set, dtype=np.uint32)
+    n = int(jfs[-1]) if len(jfs) else 0
+    b = Batch()
+    b.n_sets = n
+    b.n_jobs = len(jfs) - 1
+    b.job_first_set = jfs.ctypes.data
+    keep = [jfs]
+    if job_flags is not None:
+        fl = np.ascontiguousarray(job_flags, dtype=np.uint8)
+        keep.append(fl)
+        b.job_flags = fl.ctypes.data
+    b.seed = seed
+    out = np.zeros(max(n, 1), np.uint64)
+    rc = load().blsgpu_batch_scalars(ctypes.byref(b), out.ctypes.data)
+    if rc != OK:
+        raise RuntimeError(f"blsgpu_batch_scalars -> {code_name(rc)}")
+    return out[:n]
+
+
+def debug_inject(what, skip=0, count=1):
+    """Arms the library's fault injection (blsgpu_debug_inject): after `skip` more events, the next `count` entropy
+    draws (INJECT_ENTROPY) or pipeline runs (INJECT_DEVICE) fail.  count 0 disarms."""
+    rc = load().blsgpu_debug_inject(what, skip, count)
+    if rc != OK:
+        raise ValueError(f"blsgpu_debug_inject -> {code_name(rc)}")
 
 
 def _u8(b):

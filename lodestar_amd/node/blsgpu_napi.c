@@ -414,6 +414,25 @@ static napi_value KeyValidate(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* debugInject(what, skip, count): blsgpu_debug_inject (test hook; BLSGPU_INJECT_ENTROPY 1, BLSGPU_INJECT_DEVICE 2) */
+static napi_value DebugInject(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 3) {
+    napi_throw_type_error(env, NULL, "debugInject(what, skip, count)");
+    return NULL;
+  }
+  int32_t what = 0;
+  int64_t skip = 0, count = 0;
+  napi_get_value_int32(env, argv[0], &what);
+  napi_get_value_int64(env, argv[1], &skip);
+  napi_get_value_int64(env, argv[2], &count);
+  int rc = blsgpu_debug_inject(what, skip, count);
+  if (rc != BLSGPU_OK) return throw_code(env, "blsgpu_debug_inject", rc);
+  return NULL;
+}
+
 static napi_value ModuleInit(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"init", NULL, Init, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
@@ -426,6 +445,7 @@ static napi_value ModuleInit(napi_env env, napi_value exports) {
       {"codeName", NULL, CodeName, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"submit", NULL, Submit, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"keyValidate", NULL, KeyValidate, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
+      {"debugInject", NULL, DebugInject, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   napi_value v;

@@ -182,6 +182,34 @@ async function main() {
   }
   console.log(`ok verifySignatureSet + ${fav.cases.length} fast_aggregate_verify cases`);
 
+  // a device failure rejects every job of the call with the device status, never `false` (index.ts:368-375), and
+  // the verifier keeps serving: the next call verifies (fault injection: blsgpu_debug_inject)
+  {
+    const {addon} = require(path.join(ROOT, "lodestar_amd", "node", "BlsGpuVerifier.cjs"));
+    addon.debugInject(2, 0, 1);
+    const outs = await Promise.all([
+      settle(v.verifySignatureSets(valid.slice(0, 3), {verifyOnMainThread: true})),
+    ]);
+    for (const o of outs)
+      assert.ok(o.error && o.error.message.includes("BLSGPU_DEVICE_ERROR"), `device error: ${o.error || o.value}`);
+    addon.debugInject(2, 0, 0);
+    assert.strictEqual(await v.verifySignatureSets(valid.slice(0, 3), {verifyOnMainThread: true}), true);
+    // production scalars (seed 0: a fresh OS key per call) and their fail-closed path
+    const prod = new BlsGpuVerifier({}, {});
+    prod.uploadPubkeys(0, Uint8Array.from(table));
+    const c = fx.cases.find((x) => x.name === "multi_set_jobs/plain");
+    const po = await Promise.all(c.jobs.map((j) => settle(prod.verifySignatureSets(j.map((k) => toSet(fx.sets[k], true)),
+      {batchable: c.batchable}))));
+    po.forEach((o, ji) => expectOutcome(o, c.expected[ji], `seed-0 ${c.name} job ${ji}`));
+    addon.debugInject(1, 0, 1);
+    const ent = await settle(prod.verifySignatureSets(valid.slice(0, 3), {verifyOnMainThread: true}));
+    addon.debugInject(1, 0, 0);
+    assert.ok(ent.error && ent.error.message.includes("BLSGPU_ERR_ENTROPY"), `entropy: ${ent.error || ent.value}`);
+    assert.strictEqual(await prod.verifySignatureSets(valid.slice(0, 3), {verifyOnMainThread: true}), true);
+    await prod.close();
+    console.log("ok device error rejects (BLSGPU_DEVICE_ERROR), seed-0 scalars, entropy failure rejects");
+  }
+
   // close() rejects what is still buffered, and later calls
   const pending = settle(v.verifySignatureSets([valid[0]], {batchable: true}));
   await v.close();
