@@ -72,11 +72,12 @@ def message_variant(ctx, w, v):
     return out
 
 
-def build_workload(ctx, config, rank, world=1, n_dev=1, signer=None):
+def build_workload(ctx, config, rank, world=1, n_dev=1, signer=None, sets=0):
     """Returns dict of numpy inputs for verify_raw + description.  n_dev > 1: one call spans n_dev in-process
-    devices (the runtime shards it), so C2 carries 16,384 sets per device."""
+    devices (the runtime shards it), so C2 carries 16,384 sets per device.  sets > 0 (C1/C2 diagnostics only) overrides
+    the call size."""
     if config in ("C1", "C2"):
-        n = (128 if config == "C1" else 16384) * n_dev
+        n = (sets or (128 if config == "C1" else 16384)) * n_dev
         sks, pks = gen_keys(ctx, n)
         ctx.upload_pubkeys(0, pks)
         mkeys = [rank * n + j for j in range(n)]
@@ -466,6 +467,10 @@ def main():
                     help="on an idle device, how long a slot waits while a burst of calls keeps arriving (runtime default)")
     ap.add_argument("--miller-k", type=int, default=0,
                     help="pairings per Miller accumulator (shared squarings); 0 = the runtime's choice by run size")
+    ap.add_argument("--miller-lanes", type=int, default=0, help="lanes per pairing of one-item Miller chunks (0 = auto)")
+    ap.add_argument("--sets", type=int, default=0, help="diagnostics: sets per call of C1/C2 (default the config's)")
+    ap.add_argument("--serial", action="store_true",
+                    help="diagnostics: every branch of a run on one stream (each kernel alone on the chip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
@@ -502,7 +507,11 @@ def main():
         ctx.set_option("merge_wait_us", args.merge_wait_us)
     if args.idle_wait_us is not None:
         ctx.set_option("idle_wait_us", args.idle_wait_us)
-    work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev)
+    if args.serial:
+        ctx.set_option("serial", 1)
+    if args.miller_lanes:
+        ctx.set_option("miller_lanes", args.miller_lanes)
+    work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev, sets=args.sets)
     expected = work.pop("expected", None)
     if expected is None:
         expected = np.ones(len(work["job_first_set"]) - 1, np.int8)

@@ -154,7 +154,9 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * alternate between the device's two stream pairs, so two runs' message chains overlap and a third run's decode /
  * pubkey work fills the gaps; a deeper pipeline only queues), "merge_wait_us" (while runs are in
  * flight, a slot forming a run waits up to this long for more calls to merge, default 2000; an idle device starts
- * at once), "profile" (per-stage kernel times in
+ * at once), "miller_lanes" (lanes per pairing of the one-item-chunk Miller accumulation: 0 = by run size, the default --
+ * two lanes per pairing below 65,536 chunks, where one lane per pairing leaves SIMDs idle; 1; 2), "serial" (diagnostics: every branch of a run on one stream, so each kernel runs alone on the chip; 0/1,
+ * default 0), "profile" (per-stage kernel times in
  * blsgpu_stats.stage_ms, 0/1), "group_policy" (0 = batch groups of >= group_sets sets, the default; 1 = the
  * reference pool's grouping: calls split into <= 128-set jobs (chunkifyMaximizeChunkSize(sets, 128),
  * multithread/index.ts:156), packed into >= 128-set worker requests (prepareWork, index.ts:386-401), each
@@ -223,6 +225,7 @@ const char* blsgpu_code_name(int code);
  *     9 g2_mul_scalar_word(192,8 -> 192; out_stride >= 2880) 10 g1_mul_scalar_word(96,8 -> 96; >= 1440):
  *       the batch scalar r = a + b*lambda of a scalar word w (a = 2 lo + 1 - 2^32, b = 2 hi + 1 - 2^32 from w's
  *       32-bit halves, lambda = -z^2), word 0 = r = 1
+ *     11 fp_lc(raw limbs: 15 x 14 LE words -> 14 words): the lazily reduced combination x0 + .. + x6 - x7 - .. - x14
  * Returns BLSGPU_OK or an error. */
 int blsgpu_debug_op(blsgpu_ctx* ctx, int op, uint32_t n, const uint8_t* in, uint32_t in_stride,
                     uint8_t* out, uint32_t out_stride, int32_t* status);

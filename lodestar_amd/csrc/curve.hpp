@@ -14,6 +14,8 @@ BLS_HD fp F_neg(const fp& a) { return fp_neg(a); }
 BLS_HD bool F_is_zero(const fp& a) { return fp_is_zero(a); }
 BLS_HD fp F_select(bool c, const fp& a, const fp& b) { return fp_select(c, a, b); }
 BLS_HD fp F_add_nr(const fp& a, const fp& b) { return fp_add_nr(a, b); }
+// the operand-side sum a squaring takes: Fp one un-normalized level, Fp2 normalized (fp2_sqr's a0 - a1 needs limbs)
+BLS_HD fp F_add_sq(const fp& a, const fp& b) { return fp_add_nr(a, b); }
 BLS_HD fp2 F_add(const fp2& a, const fp2& b) { return fp2_add(a, b); }
 BLS_HD fp2 F_sub(const fp2& a, const fp2& b) { return fp2_sub(a, b); }
 BLS_HD fp2 F_mul(const fp2& a, const fp2& b) { return fp2_mul(a, b); }
@@ -23,6 +25,25 @@ BLS_HD fp2 F_neg(const fp2& a) { return fp2_neg(a); }
 BLS_HD bool F_is_zero(const fp2& a) { return fp2_is_zero(a); }
 BLS_HD fp2 F_select(bool c, const fp2& a, const fp2& b) { return fp2_select(c, a, b); }
 BLS_HD fp2 F_add_nr(const fp2& a, const fp2& b) { return fp2_add_nr(a, b); }
+BLS_HD fp2 F_add_sq(const fp2& a, const fp2& b) { return fp2_add_norm(a, b); }
+// Lazily reduced linear combinations over either field (fp.hpp fp_lc; Fp2 component-wise): F_lc(L<w>(x), ...).
+// Terms: normalized, values <= 2p (stored coordinates, products, F_lc results) -- never fp_add_nr sums.
+template <int W, class F>
+struct lt {
+  const F& v;
+};
+template <int W, class F>
+BLS_HD lt<W, F> L(const F& v) {
+  return lt<W, F>{v};
+}
+template <int... W>
+BLS_HD fp F_lc(const lt<W, fp>&... t) {
+  return fp_lc(T<W>(t.v)...);
+}
+template <int... W>
+BLS_HD fp2 F_lc(const lt<W, fp2>&... t) {
+  return fp2_make(fp_lc(T<W>(t.v.c0)...), fp_lc(T<W>(t.v.c1)...));
+}
 
 template <class F>
 struct jac {
@@ -63,8 +84,29 @@ BLS_HD jac<F> jac_from_aff(const aff<F>& a) {
   return r;
 }
 
+#ifndef BLS_LAZY_CURVE
+#define BLS_LAZY_CURVE 1
+#endif
+// The additive glue as lazily reduced combinations (F_lc); X + B goes to the squaring as F_add_sq (value <= 4p, the
+// squarings' operand contract).  D - X3 = 3 D - F.
 template <class F>
-BLS_FN jac<F> jac_dbl(const jac<F>& p) {
+BLS_FN jac<F> jac_dbl_lazy(const jac<F>& p) {
+  const F A = F_sqr(p.x);
+  const F B = F_sqr(p.y);
+  const F C = F_sqr(B);
+  const F S = F_sqr(F_add_sq(p.x, B));
+  const F D = F_lc(L<2>(S), L<-2>(A), L<-2>(C));
+  const F E = F_lc(L<3>(A));
+  const F Fv = F_sqr(E);
+  jac<F> r;
+  r.x = F_lc(L<1>(Fv), L<-2>(D));
+  const F M = F_mul(E, F_lc(L<3>(D), L<-1>(Fv)));
+  r.y = F_lc(L<1>(M), L<-8>(C));
+  r.z = F_mul(F_add_nr(p.y, p.y), p.z);
+  return r;  // infinity (z = 0) maps to z = 0
+}
+template <class F>
+BLS_FN jac<F> jac_dbl_eager(const jac<F>& p) {
   F A = F_sqr(p.x);
   F B = F_sqr(p.y);
   F C = F_sqr(B);
@@ -79,6 +121,37 @@ BLS_FN jac<F> jac_dbl(const jac<F>& p) {
   r.z = F_mul(F_add_nr(p.y, p.y), p.z);
   return r;  // infinity (z = 0) maps to z = 0
 }
+// lazy glue per group: BLS_LAZY_CURVE (both), BLS_LAZY_G1 / BLS_LAZY_G2 (one group)
+#ifndef BLS_LAZY_G1
+#define BLS_LAZY_G1 BLS_LAZY_CURVE
+#endif
+#ifndef BLS_LAZY_G2
+#define BLS_LAZY_G2 BLS_LAZY_CURVE
+#endif
+#ifndef BLS_LAZY_G2_DBL
+#define BLS_LAZY_G2_DBL BLS_LAZY_G2
+#endif
+#ifndef BLS_LAZY_G2_ADD
+#define BLS_LAZY_G2_ADD BLS_LAZY_G2
+#endif
+#ifndef BLS_LAZY_G2_ADDAFF
+#define BLS_LAZY_G2_ADDAFF BLS_LAZY_G2
+#endif
+template <class F>
+struct lazy_curve {
+  static constexpr bool dbl = BLS_LAZY_G1, add = BLS_LAZY_G1, addaff = BLS_LAZY_G1;
+};
+template <>
+struct lazy_curve<fp2> {
+  static constexpr bool dbl = BLS_LAZY_G2_DBL, add = BLS_LAZY_G2_ADD, addaff = BLS_LAZY_G2_ADDAFF;
+};
+template <class F>
+BLS_FN jac<F> jac_dbl(const jac<F>& p) {
+  if constexpr (lazy_curve<F>::dbl)
+    return jac_dbl_lazy(p);
+  else
+    return jac_dbl_eager(p);
+}
 
 template <class F>
 BLS_HD jac<F> jac_neg(const jac<F>& p) {
@@ -89,7 +162,32 @@ BLS_HD jac<F> jac_neg(const jac<F>& p) {
 
 // p + q with q affine (q never infinity here)
 template <class F>
-BLS_INL jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
+BLS_INL jac<F> jac_add_aff_lazy(const jac<F>& p, const aff<F>& q) {
+  if (jac_is_inf(p)) return jac_from_aff(q);
+  const F Z1Z1 = F_sqr(p.z);
+  const F U2 = F_mul(q.x, Z1Z1);
+  const F S2 = F_mul(q.y, F_mul(p.z, Z1Z1));
+  const F H = F_lc(L<1>(U2), L<-1>(p.x));
+  const F rr = F_lc(L<2>(S2), L<-2>(p.y));
+  if (F_is_zero(H)) {
+    if (F_is_zero(rr)) return jac_dbl(p);
+    return jac_infinity<F>();
+  }
+  const F HH = F_sqr(H);
+  const F I = F_lc(L<4>(HH));
+  const F J = F_mul(H, I);
+  const F V = F_mul(p.x, I);
+  const F R2 = F_sqr(rr);
+  jac<F> r;
+  r.x = F_lc(L<1>(R2), L<-1>(J), L<-2>(V));
+  const F M = F_mul(rr, F_lc(L<3>(V), L<-1>(R2), L<1>(J)));  // V - X3 = 3V - r^2 + J
+  const F N = F_mul(p.y, J);
+  r.y = F_lc(L<1>(M), L<-2>(N));
+  r.z = F_lc(L<1>(F_sqr(F_add_sq(p.z, H))), L<-1>(Z1Z1), L<-1>(HH));
+  return r;
+}
+template <class F>
+BLS_INL jac<F> jac_add_aff_eager(const jac<F>& p, const aff<F>& q) {
   if (jac_is_inf(p)) return jac_from_aff(q);
   F Z1Z1 = F_sqr(p.z);
   F U2 = F_mul(q.x, Z1Z1);
@@ -110,10 +208,45 @@ BLS_INL jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
   r.z = F_sub(F_sub(F_sqr(F_add(p.z, H)), Z1Z1), HH);
   return r;
 }
+template <class F>
+BLS_INL jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
+  if constexpr (lazy_curve<F>::addaff)
+    return jac_add_aff_lazy(p, q);
+  else
+    return jac_add_aff_eager(p, q);
+}
 
 // general Jacobian addition
 template <class F>
-BLS_INL jac<F> jac_add(const jac<F>& p, const jac<F>& q) {
+BLS_INL jac<F> jac_add_lazy(const jac<F>& p, const jac<F>& q) {
+  if (jac_is_inf(p)) return q;
+  if (jac_is_inf(q)) return p;
+  const F Z1Z1 = F_sqr(p.z);
+  const F Z2Z2 = F_sqr(q.z);
+  const F U1 = F_mul(p.x, Z2Z2);
+  const F U2 = F_mul(q.x, Z1Z1);
+  const F S1 = F_mul(p.y, F_mul(q.z, Z2Z2));
+  const F S2 = F_mul(q.y, F_mul(p.z, Z1Z1));
+  const F H = F_lc(L<1>(U2), L<-1>(U1));
+  const F rr = F_lc(L<2>(S2), L<-2>(S1));
+  if (F_is_zero(H)) {
+    if (F_is_zero(rr)) return jac_dbl(p);
+    return jac_infinity<F>();
+  }
+  const F I = F_sqr(F_add_sq(H, H));
+  const F J = F_mul(H, I);
+  const F V = F_mul(U1, I);
+  const F R2 = F_sqr(rr);
+  jac<F> r;
+  r.x = F_lc(L<1>(R2), L<-1>(J), L<-2>(V));
+  const F M = F_mul(rr, F_lc(L<3>(V), L<-1>(R2), L<1>(J)));  // V - X3 = 3V - r^2 + J
+  const F N = F_mul(S1, J);
+  r.y = F_lc(L<1>(M), L<-2>(N));
+  r.z = F_mul(F_lc(L<1>(F_sqr(F_add_sq(p.z, q.z))), L<-1>(Z1Z1), L<-1>(Z2Z2)), H);
+  return r;
+}
+template <class F>
+BLS_INL jac<F> jac_add_eager(const jac<F>& p, const jac<F>& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
   F Z1Z1 = F_sqr(p.z);
@@ -136,6 +269,13 @@ BLS_INL jac<F> jac_add(const jac<F>& p, const jac<F>& q) {
   r.y = F_sub(F_mul(rr, F_sub(V, r.x)), F_dbl(F_mul(S1, J)));
   r.z = F_mul(F_sub(F_sub(F_sqr(F_add(p.z, q.z)), Z1Z1), Z2Z2), H);
   return r;
+}
+template <class F>
+BLS_INL jac<F> jac_add(const jac<F>& p, const jac<F>& q) {
+  if constexpr (lazy_curve<F>::add)
+    return jac_add_lazy(p, q);
+  else
+    return jac_add_eager(p, q);
 }
 
 // [k]P for a 64-bit k, P affine (not infinity).  Left-to-right double-and-add.

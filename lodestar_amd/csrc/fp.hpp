@@ -343,6 +343,104 @@ BLS_HD fp fp_csub_p(const fp& s) {
 }
 BLS_HD fp fp_canon(const fp& a) { return fp_csub_p(fp_csub_p(a)); }
 
+// ------------------------------------------------------------------------------------------------
+// Lazily reduced linear combinations: fp_lc(T<w>(x), ...) = sum w_k x_k (mod p), reduced ONCE.
+//
+// The additive glue of the tower and point formulas (t0 + xi (X - t1 - t2), ...) is where a chain of fp_add / fp_sub
+// spends ~90 instructions per operation (carry pass + conditional 2p subtraction).  Here every term is added or
+// subtracted limb by limb in uint32 without carries, on top of a multiple K p of p whose lower 13 limbs are raised to
+// >= N (2^28 - 1) by borrowing (N = total negative weight), so no limb ever goes negative; then ONE pass subtracts
+// q p for a floor estimate q of value / p (from the top two limbs) while propagating the carries.
+// Terms: normalized limbs (< 2^28, top limb < 2^28) and values <= 2p (stored values, product outputs).  Weights
+// w in [-15, 15], total |w| <= 15 (limb sums stay below 2^32).  Result: normalized, value in [0, 1.003 p).
+// ------------------------------------------------------------------------------------------------
+struct lc_limbs {
+  uint32_t l[BLS_NL];
+};
+// K p (K = 2N: covers N negative unit terms of value <= 2p) in borrowed form: limb 0 + N 2^28, limbs 1..12 + N 2^28 -
+// N, limb 13 - N (the value is unchanged, limbs 0..12 end up >= N (2^28 - 1)).
+constexpr lc_limbs lc_ofs(int N) {
+  lc_limbs r{};
+  uint64_t c = 0;
+  for (int i = 0; i < BLS_NL; i++) {
+    const uint64_t v = (uint64_t)FP_P.l[i] * (uint64_t)(2 * N) + c;
+    r.l[i] = i < BLS_NL - 1 ? (uint32_t)(v & BLS_MASK) : (uint32_t)v;
+    c = v >> BLS_LB;
+  }
+  for (int i = 0; i < BLS_NL; i++) {
+    if (i < BLS_NL - 1) r.l[i] += (uint32_t)N << BLS_LB;
+    if (i > 0) r.l[i] -= (uint32_t)N;
+  }
+  return r;
+}
+template <int N>
+struct LcOfs {
+  static constexpr lc_limbs v = lc_ofs(N);
+};
+template <int W>
+struct lc_term {
+  const fp& x;
+};
+template <int W>
+BLS_HD lc_term<W> T(const fp& x) {
+  return lc_term<W>{x};
+}
+template <int W>
+BLS_HD void lc_apply(uint32_t* s, const lc_term<W>& t) {
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) {
+    if (W > 0)
+      s[i] += (uint32_t)W * t.x.l[i];
+    else
+      s[i] -= (uint32_t)(-W) * t.x.l[i];
+  }
+}
+template <int W>
+constexpr int lc_neg_w() {
+  return W < 0 ? -W : 0;
+}
+template <int W>
+constexpr int lc_abs_w() {
+  return W < 0 ? -W : W;
+}
+// NP = 2^392 - p in 28-bit limbs (limb 0: 2^28 - p_0, limbs 1..13: 2^28 - 1 - p_i)
+constexpr lc_limbs lc_np() {
+  lc_limbs r{};
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = (i == 0 ? (1u << BLS_LB) : BLS_MASK) - FP_P.l[i];
+  return r;
+}
+BLS_CONST lc_limbs LC_NP = lc_np();
+// s: limbs 0..12 unsigned (< 2^32), limb 13 signed; value = sum s_i 2^(28 i) >= 0 and < 64 p
+BLS_HD fp lc_reduce(const uint32_t* s) {
+  // q = floor((s13 2^28 + s12) 10080 / 2^58), 10080 = floor(2^394 / p): never above floor(value / p) (the limbs
+  // below 12 add < 2^340 and only raise the value), at most 1 below (reciprocal error 8.3e-5 relative) -> the
+  // result value is in [0, 1.003 p).  A negative top (value < 2^368) gives q = 0.
+  const int64_t vhi = (int64_t)(int32_t)s[BLS_NL - 1] * (int64_t)(1u << BLS_LB) + (int64_t)s[BLS_NL - 2];
+  const int32_t q = (int32_t)((uint64_t)(vhi > 0 ? vhi : 0) * 10080ull >> 58);
+  // v - q p = v + q (2^392 - p) - q 2^392: unsigned MADs with the limbs of NP = 2^392 - p (all in [0, 2^28)), the q 2^392
+  // leaving through the top limb (signed there).  Plain C: the same code on the device and in the host build.
+  fp r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < BLS_NL - 1; i++) {
+    acc = (acc >> BLS_LB) + (uint64_t)s[i] + (uint64_t)(uint32_t)q * (uint64_t)LC_NP.l[i];
+    r.l[i] = (uint32_t)acc & BLS_MASK;
+  }
+  r.l[BLS_NL - 1] = (uint32_t)((int64_t)(acc >> BLS_LB) + (int64_t)(int32_t)s[BLS_NL - 1] -
+                               (int64_t)q * (int64_t)(FP_P.l[BLS_NL - 1] + 1));
+  return r;
+}
+template <int... W>
+BLS_HD fp fp_lc(const lc_term<W>&... t) {
+  constexpr int N = (0 + ... + lc_neg_w<W>());
+  static_assert((0 + ... + lc_abs_w<W>()) <= 15, "fp_lc: total weight <= 15");
+  uint32_t s[BLS_NL];
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) s[i] = LcOfs<N>::v.l[i];
+  (lc_apply(s, t), ...);
+  return lc_reduce(s);
+}
+
 BLS_HD bool fp_is_zero(const fp& a) {
   fp c = fp_canon(a);
   uint32_t o = 0;

@@ -129,6 +129,18 @@ __global__ __launch_bounds__(WAVE) void k_debug_op(int op, uint32_t n, const uin
       if (st == 0) g1a_to_be96(r, o);
       break;
     }
+    case 11: {  // fp_lc of raw limbs (15 x 14 LE words): 7 positive, 8 negative unit terms -> 14 words
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(a);
+      fp x[15];
+      for (int k = 0; k < 15; k++)
+        for (int j = 0; j < BLS_NL; j++) x[k].l[j] = w[14 * k + j];
+      const fp r = fp_lc(T<1>(x[0]), T<1>(x[1]), T<1>(x[2]), T<1>(x[3]), T<1>(x[4]), T<1>(x[5]), T<1>(x[6]),
+                         T<-1>(x[7]), T<-1>(x[8]), T<-1>(x[9]), T<-1>(x[10]), T<-1>(x[11]), T<-1>(x[12]), T<-1>(x[13]),
+                         T<-1>(x[14]));
+      uint32_t* ow = reinterpret_cast<uint32_t*>(o);
+      for (int j = 0; j < BLS_NL; j++) ow[j] = r.l[j];
+      break;
+    }
     default:
       st = -2;
   }

@@ -12,6 +12,17 @@
 #include "k_common.hpp"
 #include "gt_wave.hpp"
 
+// lane-pair exchange (lane ^ 1) of register values: __shfl_xor, no LDS
+BLS_INL fp fp_xlane(const fp& x) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = (uint32_t)__shfl_xor((int)x.l[i], 1);
+  return r;
+}
+BLS_INL fp2 fp2_xlane(const fp2& x) { return fp2_make(fp_xlane(x.c0), fp_xlane(x.c1)); }
+BLS_INL fp6 fp6_xlane(const fp6& x) { return fp6_make(fp2_xlane(x.c0), fp2_xlane(x.c1), fp2_xlane(x.c2)); }
+BLS_INL fp fp_add_n(const fp& a, const fp& b) { return fp_add_norm(a, b); }
+
 STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_miller_lines(PipelineBuffers b) {
   uint32_t u = blockIdx.x * WAVE + threadIdx.x;
   if (u >= b.n_umsg || (b.mflags[u] & MF_H_INF)) return;
@@ -37,6 +48,64 @@ STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_miller_lines(PipelineBuffers b) {
     st_fp2(o, b.nm, u, 0, L.l0);
     st_fp2(o, b.nm, u, 2 * W_FP, L.c1);
     st_fp2(o, b.nm, u, 4 * W_FP, L.c4);
+  }
+}
+
+// The same lines on TWO lanes per message (mid-size runs, latency): both lanes hold T; a doubling step's products run
+// as two phases of independent products split over the pair (phase 1: lane 0 X Y, Y^2, X^2 | lane 1 Z^2, (Y + Z)^2;
+// phase 2: lane 0 A (B - F), B H | lane 1 E^2, G^2), the partner's results arriving by lane exchanges: 5 product
+// times per doubling instead of 9.  The five addition steps run on both lanes.  Lane h stores word half h of the line.
+STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_miller_lines2(PipelineBuffers b) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  const uint32_t u = q >> 1, h = q & 1;
+  if (u >= b.n_umsg || (b.mflags[u] & MF_H_INF)) return;  // both lanes of a pair leave together
+  const g2a Q = ld_g2a(b.h_aff, b.nm, u);
+  g2proj Tp;
+  Tp.x = Q.x;
+  Tp.y = Q.y;
+  Tp.z = fp2_one();
+  int bit = 62;
+  bool add_next = false;
+#pragma unroll 1
+  for (int s = 0; s < MILLER_STEPS; s++) {
+    line3 Ln;
+    if (!add_next) {
+      // phase 1
+      const fp2 p0 = fp2_mul(h ? Tp.z : Tp.x, h ? Tp.z : Tp.y);          // lane 0: X Y      lane 1: Z^2
+      const fp2 p1 = fp2_sqr(h ? fp2_add_norm(Tp.y, Tp.z) : Tp.y);      // lane 0: Y^2      lane 1: (Y + Z)^2
+      const fp2 p2 = fp2_sqr(Tp.x);                                    // lane 0: X^2      (lane 1: unused)
+      const fp2 o0 = fp2_xlane(p0), o1 = fp2_xlane(p1), o2 = fp2_xlane(p2);
+      const fp2 XY = h ? o0 : p0, C = h ? p0 : o0, B = h ? o1 : p1, S = h ? p1 : o1, J = h ? o2 : p2;
+      const fp2 A = fp2_half(XY);
+      const fp2 xC = fp2_make(fp_lc(T<1>(C.c0), T<-1>(C.c1)), fp_lc(T<1>(C.c0), T<1>(C.c1)));
+      const fp2 E = F_lc(L<12>(xC));
+      const fp2 G = fp2_half(F_lc(L<1>(B), L<3>(E)));
+      const fp2 H = F_lc(L<1>(S), L<-1>(B), L<-1>(C));
+      // phase 2
+      const fp2 q0 = fp2_mul(h ? E : A, h ? E : F_lc(L<1>(B), L<-3>(E)));  // lane 0: A (B - F)   lane 1: E^2
+      const fp2 q1 = fp2_mul(h ? G : B, h ? G : H);                       // lane 0: B H         lane 1: G^2
+      const fp2 r0 = fp2_xlane(q0), r1 = fp2_xlane(q1);
+      const fp2 E2 = h ? q0 : r0, G2 = h ? q1 : r1;
+      Tp.x = h ? r0 : q0;
+      Tp.z = h ? r1 : q1;
+      Tp.y = F_lc(L<1>(G2), L<-3>(E2));
+      Ln.l0 = F_lc(L<1>(E), L<-1>(B));
+      Ln.c1 = F_lc(L<3>(J));
+      Ln.c4 = F_lc(L<-1>(H));
+      add_next = (BLS_Z_ABS >> bit) & 1ull;
+      bit--;
+    } else {
+      miller_add_line(Tp, Q, Ln);
+      add_next = false;
+    }
+    uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
+    if (h) {
+      st_fp(o, b.nm, u, 3 * W_FP, Ln.c1.c1);
+      st_fp2(o, b.nm, u, 4 * W_FP, Ln.c4);
+    } else {
+      st_fp2(o, b.nm, u, 0, Ln.l0);
+      st_fp(o, b.nm, u, 2 * W_FP, Ln.c1.c0);
+    }
   }
 }
 
@@ -86,6 +155,96 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc(PipelineBuffers b) {
   st_fp12(b.f_chunk, b.n, c, fp12_conj(f));
 }
 
+// Mid-size runs (latency with the chip not filled by one lane per pairing): TWO lanes per pairing, lane h of the
+// pair holding half c_h of f = c0 + c1 w (Fp6 each) and the partner's half arriving by a lane exchange (__shfl_xor,
+// no LDS).  Per step each lane does one Fp6 product of the complex squaring (lane 0: t = c0 c1, lane 1:
+// s = (c0 + c1)(c0 + v c1); then c1' = 2t, c0' = s - t - v t) and one half of the sparse line product
+// (c0' = c0 L01 + v (c1 l4 v), c1' = c1 L01 + c0 (l4 v)): 14 Fp2 products per lane per step against 25 on one lane, so
+// a pairing takes ~0.56 of the lane-per-pairing time (12% more work in all).  One item per chunk.
+template <bool UNITS>
+STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc2(PipelineBuffers b) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  const uint32_t c = q >> 1, h = q & 1;  // both lanes of a pair see the same c (WAVE is even)
+  if (c >= b.n_chunks) return;           // whole pairs leave together: the exchanges below stay within live pairs
+  const uint32_t i = b.chunk_items[b.chunk_first[c]];
+  uint32_t m;
+  bool active;
+  if (UNITS) {
+    m = b.unit_msg[i];
+    active = b.unit_ok[i] != 0;
+  } else {
+    m = b.msg_idx[i];
+    active = b.include[i] != 0;
+  }
+  active = active && !(b.mflags[m] & MF_H_INF);  // the same on both lanes of the pair
+  g1a P;
+  if (active) P = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
+  fp6 mine = h ? fp6_zero() : fp6_one();
+  int bit = 62;
+  bool add_next = false;
+#pragma unroll 1
+  for (int s = 0; s < MILLER_STEPS && active; s++) {
+    if (!add_next && s != 0) {
+      const fp6 other = fp6_xlane(mine);
+      const fp6 a0 = h ? other : mine, a1 = h ? mine : other;
+      fp6 X, Y;  // lane 0: (a0, a1); lane 1: (a0 + a1, a0 + v a1), normalized, values <= 4p (fp6_mul's contract)
+      if (h) {
+        X.c0 = fp2_make(fp_add_n(a0.c0.c0, a1.c0.c0), fp_add_n(a0.c0.c1, a1.c0.c1));
+        X.c1 = fp2_make(fp_add_n(a0.c1.c0, a1.c1.c0), fp_add_n(a0.c1.c1, a1.c1.c1));
+        X.c2 = fp2_make(fp_add_n(a0.c2.c0, a1.c2.c0), fp_add_n(a0.c2.c1, a1.c2.c1));
+        Y.c0 = fp2_make(fp_lc(T<1>(a0.c0.c0), T<1>(a1.c2.c0), T<-1>(a1.c2.c1)),
+                        fp_lc(T<1>(a0.c0.c1), T<1>(a1.c2.c0), T<1>(a1.c2.c1)));
+        Y.c1 = fp2_make(fp_add_n(a0.c1.c0, a1.c0.c0), fp_add_n(a0.c1.c1, a1.c0.c1));
+        Y.c2 = fp2_make(fp_add_n(a0.c2.c0, a1.c1.c0), fp_add_n(a0.c2.c1, a1.c1.c1));
+      } else {
+        X = a0;
+        Y = a1;
+      }
+      const fp6 pr = fp6_mul(X, Y);
+      const fp6 t = fp6_xlane(pr);  // lane 1 receives t = a0 a1
+      fp6 r;
+      if (h) {  // c0' = s - t - v t, v t = (xi t2, t0, t1)
+        r.c0.c0 = fp_lc(T<1>(pr.c0.c0), T<-1>(t.c0.c0), T<-1>(t.c2.c0), T<1>(t.c2.c1));
+        r.c0.c1 = fp_lc(T<1>(pr.c0.c1), T<-1>(t.c0.c1), T<-1>(t.c2.c0), T<-1>(t.c2.c1));
+        r.c1.c0 = fp_lc(T<1>(pr.c1.c0), T<-1>(t.c1.c0), T<-1>(t.c0.c0));
+        r.c1.c1 = fp_lc(T<1>(pr.c1.c1), T<-1>(t.c1.c1), T<-1>(t.c0.c1));
+        r.c2.c0 = fp_lc(T<1>(pr.c2.c0), T<-1>(t.c2.c0), T<-1>(t.c1.c0));
+        r.c2.c1 = fp_lc(T<1>(pr.c2.c1), T<-1>(t.c2.c1), T<-1>(t.c1.c1));
+      } else {  // c1' = 2t
+        r.c0 = fp2_make(fp_lc(T<2>(pr.c0.c0)), fp_lc(T<2>(pr.c0.c1)));
+        r.c1 = fp2_make(fp_lc(T<2>(pr.c1.c0)), fp_lc(T<2>(pr.c1.c1)));
+        r.c2 = fp2_make(fp_lc(T<2>(pr.c2.c0)), fp_lc(T<2>(pr.c2.c1)));
+      }
+      mine = fp6_xlane(r);  // lane 0 computed c1', lane 1 c0': swap back
+    }
+    const uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
+    const fp2 l0 = ld_fp2(o, b.nm, m, 0);
+    const fp2 l1 = fp2_mul_fp(ld_fp2(o, b.nm, m, 2 * W_FP), P.x);
+    const fp2 l4 = fp2_mul_fp(ld_fp2(o, b.nm, m, 4 * W_FP), P.y);
+    // lane 0: c0' = c0 (l0 + l1 v) + v (c1 (l4 v)); lane 1: c1' = c1 (l0 + l1 v) + c0 (l4 v)
+    const fp6 other = fp6_xlane(mine);
+    const fp6 A = fp6_mul_by_01(mine, l0, l1);  // own half times (l0 + l1 v)
+    const fp6 Z = fp6_mul_by_1(other, l4);
+    const fp6 Zv = h ? Z : fp6_mul_v(Z);
+    fp6 r;
+    r.c0 = fp2_make(fp_lc(T<1>(A.c0.c0), T<1>(Zv.c0.c0)), fp_lc(T<1>(A.c0.c1), T<1>(Zv.c0.c1)));
+    r.c1 = fp2_make(fp_lc(T<1>(A.c1.c0), T<1>(Zv.c1.c0)), fp_lc(T<1>(A.c1.c1), T<1>(Zv.c1.c1)));
+    r.c2 = fp2_make(fp_lc(T<1>(A.c2.c0), T<1>(Zv.c2.c0)), fp_lc(T<1>(A.c2.c1), T<1>(Zv.c2.c1)));
+    mine = r;
+    if (!add_next) {
+      add_next = (BLS_Z_ABS >> bit) & 1ull;
+      bit--;
+    } else {
+      add_next = false;
+    }
+  }
+  // f_chunk[c] = conj(f) = (c0, -c1): lane h writes its half (words 6 h W_FP .. )
+  const fp6 out = h ? fp6_neg(mine) : mine;
+  st_fp2(b.f_chunk, b.n, c, 6 * (int)h * W_FP, out.c0);
+  st_fp2(b.f_chunk, b.n, c, (6 * (int)h + 2) * W_FP, out.c1);
+  st_fp2(b.f_chunk, b.n, c, (6 * (int)h + 4) * W_FP, out.c2);
+}
+
 // Small runs (latency): one 128-lane workgroup per pairing, the Miller loop as cooperative Fp12 arithmetic
 // (gt_wave.hpp: lines computed on the fly, one Fp product per lane per step) -- the same value as
 // k_miller_lines + k_miller_acc with one item per chunk, in ~1/6 of the time per pairing, at a fraction of the
@@ -132,6 +291,16 @@ void launch_miller_coop(const PipelineBuffers& b, bool units, hipStream_t s, boo
 
 void launch_miller_lines(const PipelineBuffers& b, hipStream_t s) {
   if (b.n_umsg) hipLaunchKernelGGL(k_miller_lines, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
+}
+void launch_miller_lines2(const PipelineBuffers& b, hipStream_t s) {
+  if (b.n_umsg) hipLaunchKernelGGL(k_miller_lines2, grid_for(2 * b.n_umsg), dim3(WAVE), 0, s, b);
+}
+void launch_miller_acc2(const PipelineBuffers& b, bool units, hipStream_t s) {
+  if (!b.n_chunks) return;
+  if (units)
+    hipLaunchKernelGGL(k_miller_acc2<true>, grid_for(2 * b.n_chunks), dim3(WAVE), 0, s, b);
+  else
+    hipLaunchKernelGGL(k_miller_acc2<false>, grid_for(2 * b.n_chunks), dim3(WAVE), 0, s, b);
 }
 void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s) {
   if (!b.n_chunks) return;

@@ -196,9 +196,11 @@ struct Options {  // snapshot taken at the start of each call
   int64_t idle_wait_us = 0;  // on an idle device, a slot waits up to this long while calls keep arriving (bursts)
   int64_t pipeline_depth = 3;    // runs a device has in flight (taken by a slot, batch pass not yet complete)
   int64_t group_policy = 0;    // 0 = groups of >= group_sets sets; 1 = the reference pool's jobs / requests / chunks
+  bool serial = false;  // diagnostics: every branch of a run on one stream (each kernel alone on the chip)
+  int64_t miller_lanes = 0;  // lanes per pairing of the one-item-chunk Miller accumulation: 0 = by run size, 1, 2
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
-           group_policy == o.group_policy;
+           group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes;
   }
 };
 
@@ -225,6 +227,16 @@ inline uint32_t miller_k_auto(uint32_t n_items) {
   uint32_t k = 1;
   while (k < 4 && n_items / (2 * k) >= 65536) k *= 2;
   return k;
+}
+
+// The Miller accumulation of a run's chunks: two lanes per pairing (k_miller_acc2) when the chunks hold one item each
+// and one lane per chunk would leave SIMDs idle (< 65,536 chunks = 1,024 waves), else one lane per chunk.
+void launch_miller_acc_auto(const PipelineBuffers& pb, bool units, hipStream_t st, uint32_t mk, int64_t lanes_opt) {
+  const bool two = lanes_opt == 2 || (lanes_opt == 0 && mk == 1 && pb.n_chunks < 65536);
+  if (two && mk == 1)
+    launch_miller_acc2(pb, units, st);
+  else
+    launch_miller_acc(pb, units, st);
 }
 
 // Splits item ranges into Miller chunks of <= k items: appends to first/items, returns [chunk_begin, end)
@@ -710,13 +722,14 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // short next to the message branch; see sp below for small runs) and consecutive runs use the other pair; without,
   // each branch has its own stream shared by every run.
   const bool prof = opt.profile;
-  const bool spec = BLSGPU_STREAM_PAIRS && coop && sl.alone;  // speculative MSM (below)
+  const bool spec = BLSGPU_STREAM_PAIRS && coop && sl.alone && !opt.serial;  // speculative MSM (below)
   // A small run that found the device idle puts its pubkey branch on the other pair's (idle) signature stream, beside
   // its own signature decode and subgroup checks instead of in front of them: the signature branch was a small
   // call's critical path (C1 serial trace: 7.25 ms vs the message branch's 6.15).
   hipStream_t sm = BLSGPU_STREAM_PAIRS ? d.st[2 * par + 1] : d.st[kMsg],
               sp = BLSGPU_STREAM_PAIRS ? (coop && sl.alone ? d.st[2 * (1 - par)] : s) : d.st[kPk],
               stl = BLSGPU_STREAM_PAIRS ? s : d.st[kTail];
+  if (opt.serial) sm = sp = stl = s;
   auto beg = [&](int k, hipStream_t st) {
     if (prof) HIPCHK(hipEventRecord(sl.ev[2 * k], st));
   };
@@ -735,7 +748,14 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     launch_h_affine(pb, sm);
     end(1, sm);
     beg(kStages, sm);
-    if (!coop) launch_miller_lines(pb, sm);
+    if (!coop) {
+      // two lanes per message while one lane each would leave SIMDs idle (the same rule as the accumulation's)
+      const bool two = opt.miller_lanes == 2 || (opt.miller_lanes == 0 && n_umsg < 65536);
+      if (two)
+        launch_miller_lines2(pb, sm);
+      else
+        launch_miller_lines(pb, sm);
+    }
     end(kStages, sm);
     // pubkeys
     beg(2, sp);
@@ -779,7 +799,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     if (coop)
       launch_miller_coop(pb, merged, sm, BLSGPU_EXCLUSIVE_SMALL);
     else
-      launch_miller_acc(pb, merged, sm);
+      launch_miller_acc_auto(pb, merged, sm, mk, opt.miller_lanes);
     end(5, sm);
     const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
     beg(6, sm);
@@ -954,7 +974,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     if (coop)  // no stored lines in a cooperative run: the per-job chunks hold one set each (mk = 1)
       launch_miller_coop(pr, false, stl);
     else
-      launch_miller_acc(pr, false, stl);
+      launch_miller_acc_auto(pr, false, stl, mk, opt.miller_lanes);
     if (small_jobs) {
       // r_i sig_i for the retried sets (G2 window tables and results in the fallback's own buffers)
       sl.d_fb.ensure((size_t)stride * 9 * W_G2J);
@@ -1807,6 +1827,11 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "pipeline_depth") {
     if (value < 1 || value > 64) return BLSGPU_ERR_ARGS;
     ctx->opt.pipeline_depth = value;
+  } else if (k == "serial") {
+    ctx->opt.serial = value != 0;
+  } else if (k == "miller_lanes") {
+    if (value < 0 || value > 2) return BLSGPU_ERR_ARGS;
+    ctx->opt.miller_lanes = value;
   } else {
     return BLSGPU_ERR_ARGS;
   }
@@ -1847,6 +1872,8 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "merge_wait_us") *value = o.merge_wait_us;
   else if (k == "idle_wait_us") *value = o.idle_wait_us;
   else if (k == "pipeline_depth") *value = o.pipeline_depth;
+  else if (k == "serial") *value = o.serial;
+  else if (k == "miller_lanes") *value = o.miller_lanes;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }

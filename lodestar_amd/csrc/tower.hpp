@@ -26,6 +26,8 @@ BLS_HD fp2 fp2_dbl(const fp2& a) { return fp2_make(fp_dbl(a.c0), fp_dbl(a.c1)); 
 BLS_HD fp2 fp2_half(const fp2& a) { return fp2_make(fp_half(a.c0), fp_half(a.c1)); }
 BLS_HD fp2 fp2_conj(const fp2& a) { return fp2_make(a.c0, fp_neg(a.c1)); }
 BLS_HD fp2 fp2_add_nr(const fp2& a, const fp2& b) { return fp2_make(fp_add_nr(a.c0, b.c0), fp_add_nr(a.c1, b.c1)); }
+// carries propagated, no reduction: the operand-side sum an Fp2 squaring takes (normalized, value <= a + b <= 4p)
+BLS_HD fp2 fp2_add_norm(const fp2& a, const fp2& b) { return fp2_make(fp_add_norm(a.c0, b.c0), fp_add_norm(a.c1, b.c1)); }
 
 // 64 p^2 in 28 limbs of 28 bits: the multiple of p added to a0 b0 - a1 b1 in fp2_mul_lazy_body so the c0 column sum
 // stays a non-negative integer for inputs < 8p (a1 b1 < 64 p^2)
@@ -88,9 +90,11 @@ BLS_INL fp2 fp2_mul_lazy_body(const fp& a0, const fp& a1, const fp& b0, const fp
   return r;
 }
 
-// Fp2 squaring (complex method): c0 = (a0 + a1)(a0 - a1), c1 = 2 a0 a1 -- two independent products.
+// Fp2 squaring (complex method): c0 = (a0 + a1)(a0 - a1), c1 = 2 a0 a1 -- two independent products.  Input:
+// normalized limbs, values <= 4p (stored values, or fp2_add_norm of two); a0 - a1 goes to the product as
+// a0 + 8p - a1 (fp_sub_k8, no reduction), so an input above 2p never underflows.  Outputs < 1.05 p.
 BLS_INL fp2 fp2_sqr_body(const fp2& a) {
-  const fp c0 = fp_mul_body(fp_add_nr(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  const fp c0 = fp_mul_body(fp_add_nr(a.c0, a.c1), fp_sub_k8(a.c0, a.c1));
   const fp c1 = fp_mul_body(fp_add_nr(a.c0, a.c0), a.c1);
   return fp2_make(c0, c1);
 }
@@ -198,7 +202,7 @@ BLS_FN fp2 fp2_mul(const fp2& a, const fp2& b) {
   return fp2_make(fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1));
 }
 BLS_FN fp2 fp2_sqr(const fp2& a) {
-  fp c0 = fp_mul(fp_add_nr(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  fp c0 = fp_mul(fp_add_nr(a.c0, a.c1), fp_sub_k8(a.c0, a.c1));
   fp c1 = fp_mul(fp_add_nr(a.c0, a.c0), a.c1);
   return fp2_make(c0, c1);
 }
@@ -280,25 +284,93 @@ BLS_FN fp6 fp6_sub(const fp6& a, const fp6& b) { return fp6_make(fp2_sub(a.c0, b
 BLS_FN fp6 fp6_neg(const fp6& a) { return fp6_make(fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)); }
 BLS_FN fp6 fp6_mul_v(const fp6& a) { return fp6_make(fp2_mul_xi(a.c2), a.c0, a.c1); }
 
+// Karatsuba over Fp2: six Fp2 products.  The operand sums go to fp2_mul un-normalized (fp2_add_nr): a, b are
+// normalized with values <= 4p, so the sums have limbs < 2^29 and values <= 8p -- fp2_mul's input contract.  With
+// BLS_LAZY_TOWER each output Fp component is ONE lazily reduced linear combination of product components (fp_lc):
+//   c0 = t0 + xi (X - t1 - t2),  c1 = Y - t0 - t1 + xi t2,  c2 = Z - t0 - t2 + t1   (xi (x0 + x1 u) = (x0 - x1) + (x0 + x1) u)
+#ifndef BLS_LAZY_TOWER
+#define BLS_LAZY_TOWER 1
+#endif
+#ifndef BLS_LAZY_FP6
+#define BLS_LAZY_FP6 BLS_LAZY_TOWER
+#endif
+#ifndef BLS_LAZY_SQR
+#define BLS_LAZY_SQR BLS_LAZY_TOWER
+#endif
+#ifndef BLS_LAZY_014
+#define BLS_LAZY_014 BLS_LAZY_TOWER
+#endif
+#if BLS_LAZY_FP6
+BLS_FN fp6 fp6_mul(const fp6& a, const fp6& b) {
+  const fp2 t0 = fp2_mul(a.c0, b.c0);
+  const fp2 t1 = fp2_mul(a.c1, b.c1);
+  const fp2 t2 = fp2_mul(a.c2, b.c2);
+  fp6 r;
+  {
+    const fp2 X = fp2_mul(fp2_add_nr(a.c1, a.c2), fp2_add_nr(b.c1, b.c2));
+    r.c0.c0 = fp_lc(T<1>(t0.c0), T<1>(X.c0), T<-1>(t1.c0), T<-1>(t2.c0), T<-1>(X.c1), T<1>(t1.c1), T<1>(t2.c1));
+    r.c0.c1 = fp_lc(T<1>(t0.c1), T<1>(X.c0), T<-1>(t1.c0), T<-1>(t2.c0), T<1>(X.c1), T<-1>(t1.c1), T<-1>(t2.c1));
+  }
+  {
+    const fp2 Y = fp2_mul(fp2_add_nr(a.c0, a.c1), fp2_add_nr(b.c0, b.c1));
+    r.c1.c0 = fp_lc(T<1>(Y.c0), T<-1>(t0.c0), T<-1>(t1.c0), T<1>(t2.c0), T<-1>(t2.c1));
+    r.c1.c1 = fp_lc(T<1>(Y.c1), T<-1>(t0.c1), T<-1>(t1.c1), T<1>(t2.c0), T<1>(t2.c1));
+  }
+  {
+    const fp2 Z = fp2_mul(fp2_add_nr(a.c0, a.c2), fp2_add_nr(b.c0, b.c2));
+    r.c2.c0 = fp_lc(T<1>(Z.c0), T<-1>(t0.c0), T<-1>(t2.c0), T<1>(t1.c0));
+    r.c2.c1 = fp_lc(T<1>(Z.c1), T<-1>(t0.c1), T<-1>(t2.c1), T<1>(t1.c1));
+  }
+  return r;
+}
+#else
 BLS_FN fp6 fp6_mul(const fp6& a, const fp6& b) {
   fp2 t0 = fp2_mul(a.c0, b.c0);
   fp2 t1 = fp2_mul(a.c1, b.c1);
   fp2 t2 = fp2_mul(a.c2, b.c2);
-  fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), fp2_add(t1, t2))));
-  fp2 c1 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
-  fp2 c2 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+  fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add_nr(a.c1, a.c2), fp2_add_nr(b.c1, b.c2)), fp2_add(t1, t2))));
+  fp2 c1 = fp2_add(fp2_sub(fp2_mul(fp2_add_nr(a.c0, a.c1), fp2_add_nr(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
+  fp2 c2 = fp2_add(fp2_sub(fp2_mul(fp2_add_nr(a.c0, a.c2), fp2_add_nr(b.c0, b.c2)), fp2_add(t0, t2)), t1);
   return fp6_make(c0, c1, c2);
 }
 
-// (x0 + x1 v + x2 v^2)(l0 + l1 v)
+#endif
+
+// (x0 + x1 v + x2 v^2)(l0 + l1 v): t0 = x0 l0, t1 = x1 l1, c0 = t0 + xi (x2 l1), c1 = (x0 + x1)(l0 + l1) - t0 - t1,
+// c2 = x2 l0 + t1 -- five Fp2 products (x, l normalized, values <= 4p)
+#if BLS_LAZY_FP6
+BLS_FN fp6 fp6_mul_by_01(const fp6& x, const fp2& l0, const fp2& l1) {
+  const fp2 t0 = fp2_mul(x.c0, l0);
+  const fp2 t1 = fp2_mul(x.c1, l1);
+  fp6 r;
+  {
+    const fp2 u = fp2_mul(x.c2, l1);
+    r.c0.c0 = fp_lc(T<1>(t0.c0), T<1>(u.c0), T<-1>(u.c1));
+    r.c0.c1 = fp_lc(T<1>(t0.c1), T<1>(u.c0), T<1>(u.c1));
+  }
+  {
+    const fp2 v = fp2_mul(fp2_add_nr(x.c0, x.c1), fp2_add_nr(l0, l1));
+    r.c1.c0 = fp_lc(T<1>(v.c0), T<-1>(t0.c0), T<-1>(t1.c0));
+    r.c1.c1 = fp_lc(T<1>(v.c1), T<-1>(t0.c1), T<-1>(t1.c1));
+  }
+  {
+    const fp2 w = fp2_mul(x.c2, l0);
+    r.c2.c0 = fp_lc(T<1>(w.c0), T<1>(t1.c0));
+    r.c2.c1 = fp_lc(T<1>(w.c1), T<1>(t1.c1));
+  }
+  return r;
+}
+#else
 BLS_FN fp6 fp6_mul_by_01(const fp6& x, const fp2& l0, const fp2& l1) {
   fp2 t0 = fp2_mul(x.c0, l0);
   fp2 t1 = fp2_mul(x.c1, l1);
   fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(x.c2, l1)));
-  fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(x.c0, x.c1), fp2_add(l0, l1)), t0), t1);
+  fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_nr(x.c0, x.c1), fp2_add_nr(l0, l1)), t0), t1);  // (see fp6_mul)
   fp2 c2 = fp2_add(fp2_mul(x.c2, l0), t1);
   return fp6_make(c0, c1, c2);
 }
+
+#endif
 
 // (x0 + x1 v + x2 v^2) * (l1 v)
 BLS_FN fp6 fp6_mul_by_1(const fp6& x, const fp2& l1) {
@@ -323,6 +395,34 @@ BLS_HD fp12 fp12_make(const fp6& a, const fp6& b) {
 }
 BLS_HD fp12 fp12_one() { return fp12_make(fp6_one(), fp6_zero()); }
 
+#if BLS_LAZY_FP6
+// Karatsuba over Fp6 (fp6_mul's lazy contract: operand sums normalized, not reduced, values <= 4p);
+// c0 = t0 + v t1 = (t0.c0 + xi t1.c2, t0.c1 + t1.c0, t0.c2 + t1.c1), c1 = X - t0 - t1.
+BLS_FN fp12 fp12_mul(const fp12& a, const fp12& b) {
+  const fp6 t0 = fp6_mul(a.c0, b.c0);
+  const fp6 t1 = fp6_mul(a.c1, b.c1);
+  fp6 sa, sb;
+  sa.c0 = fp2_make(fp_add_norm(a.c0.c0.c0, a.c1.c0.c0), fp_add_norm(a.c0.c0.c1, a.c1.c0.c1));
+  sa.c1 = fp2_make(fp_add_norm(a.c0.c1.c0, a.c1.c1.c0), fp_add_norm(a.c0.c1.c1, a.c1.c1.c1));
+  sa.c2 = fp2_make(fp_add_norm(a.c0.c2.c0, a.c1.c2.c0), fp_add_norm(a.c0.c2.c1, a.c1.c2.c1));
+  sb.c0 = fp2_make(fp_add_norm(b.c0.c0.c0, b.c1.c0.c0), fp_add_norm(b.c0.c0.c1, b.c1.c0.c1));
+  sb.c1 = fp2_make(fp_add_norm(b.c0.c1.c0, b.c1.c1.c0), fp_add_norm(b.c0.c1.c1, b.c1.c1.c1));
+  sb.c2 = fp2_make(fp_add_norm(b.c0.c2.c0, b.c1.c2.c0), fp_add_norm(b.c0.c2.c1, b.c1.c2.c1));
+  const fp6 X = fp6_mul(sa, sb);
+  fp12 r;
+  r.c0.c0 = fp2_make(fp_lc(T<1>(t0.c0.c0), T<1>(t1.c2.c0), T<-1>(t1.c2.c1)),
+                     fp_lc(T<1>(t0.c0.c1), T<1>(t1.c2.c0), T<1>(t1.c2.c1)));
+  r.c0.c1 = fp2_make(fp_lc(T<1>(t0.c1.c0), T<1>(t1.c0.c0)), fp_lc(T<1>(t0.c1.c1), T<1>(t1.c0.c1)));
+  r.c0.c2 = fp2_make(fp_lc(T<1>(t0.c2.c0), T<1>(t1.c1.c0)), fp_lc(T<1>(t0.c2.c1), T<1>(t1.c1.c1)));
+  r.c1.c0 = fp2_make(fp_lc(T<1>(X.c0.c0), T<-1>(t0.c0.c0), T<-1>(t1.c0.c0)),
+                     fp_lc(T<1>(X.c0.c1), T<-1>(t0.c0.c1), T<-1>(t1.c0.c1)));
+  r.c1.c1 = fp2_make(fp_lc(T<1>(X.c1.c0), T<-1>(t0.c1.c0), T<-1>(t1.c1.c0)),
+                     fp_lc(T<1>(X.c1.c1), T<-1>(t0.c1.c1), T<-1>(t1.c1.c1)));
+  r.c1.c2 = fp2_make(fp_lc(T<1>(X.c2.c0), T<-1>(t0.c2.c0), T<-1>(t1.c2.c0)),
+                     fp_lc(T<1>(X.c2.c1), T<-1>(t0.c2.c1), T<-1>(t1.c2.c1)));
+  return r;
+}
+#else
 BLS_FN fp12 fp12_mul(const fp12& a, const fp12& b) {
   fp6 t0 = fp6_mul(a.c0, b.c0);
   fp6 t1 = fp6_mul(a.c1, b.c1);
@@ -330,8 +430,37 @@ BLS_FN fp12 fp12_mul(const fp12& a, const fp12& b) {
   fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
   return fp12_make(c0, c1);
 }
+#endif
 
 // (a0 + a1 w)^2 = (a0^2 + v a1^2) + 2 a0 a1 w ;  complex-method squaring, 2 Fp6 muls
+#if BLS_LAZY_SQR
+// u = a0 + a1 and w = a0 + v a1 as fp6_mul operands (normalized, values <= 4p: carry pass only, no reduction, except
+// w.c0 = a0.c0 + xi a1.c2, a signed combination); c0 = s - t - v t, c1 = 2 t as combinations of the reduced s, t.
+BLS_FN fp12 fp12_sqr(const fp12& a) {
+  const fp6 t = fp6_mul(a.c0, a.c1);
+  fp6 u, w;
+  u.c0 = fp2_make(fp_add_norm(a.c0.c0.c0, a.c1.c0.c0), fp_add_norm(a.c0.c0.c1, a.c1.c0.c1));
+  u.c1 = fp2_make(fp_add_norm(a.c0.c1.c0, a.c1.c1.c0), fp_add_norm(a.c0.c1.c1, a.c1.c1.c1));
+  u.c2 = fp2_make(fp_add_norm(a.c0.c2.c0, a.c1.c2.c0), fp_add_norm(a.c0.c2.c1, a.c1.c2.c1));
+  w.c0 = fp2_make(fp_lc(T<1>(a.c0.c0.c0), T<1>(a.c1.c2.c0), T<-1>(a.c1.c2.c1)),
+                  fp_lc(T<1>(a.c0.c0.c1), T<1>(a.c1.c2.c0), T<1>(a.c1.c2.c1)));
+  w.c1 = fp2_make(fp_add_norm(a.c0.c1.c0, a.c1.c0.c0), fp_add_norm(a.c0.c1.c1, a.c1.c0.c1));
+  w.c2 = fp2_make(fp_add_norm(a.c0.c2.c0, a.c1.c1.c0), fp_add_norm(a.c0.c2.c1, a.c1.c1.c1));
+  const fp6 s = fp6_mul(u, w);
+  fp12 r;
+  // v t = (xi t2, t0, t1)
+  r.c0.c0.c0 = fp_lc(T<1>(s.c0.c0), T<-1>(t.c0.c0), T<-1>(t.c2.c0), T<1>(t.c2.c1));
+  r.c0.c0.c1 = fp_lc(T<1>(s.c0.c1), T<-1>(t.c0.c1), T<-1>(t.c2.c0), T<-1>(t.c2.c1));
+  r.c0.c1.c0 = fp_lc(T<1>(s.c1.c0), T<-1>(t.c1.c0), T<-1>(t.c0.c0));
+  r.c0.c1.c1 = fp_lc(T<1>(s.c1.c1), T<-1>(t.c1.c1), T<-1>(t.c0.c1));
+  r.c0.c2.c0 = fp_lc(T<1>(s.c2.c0), T<-1>(t.c2.c0), T<-1>(t.c1.c0));
+  r.c0.c2.c1 = fp_lc(T<1>(s.c2.c1), T<-1>(t.c2.c1), T<-1>(t.c1.c1));
+  r.c1.c0 = fp2_make(fp_lc(T<2>(t.c0.c0)), fp_lc(T<2>(t.c0.c1)));
+  r.c1.c1 = fp2_make(fp_lc(T<2>(t.c1.c0)), fp_lc(T<2>(t.c1.c1)));
+  r.c1.c2 = fp2_make(fp_lc(T<2>(t.c2.c0)), fp_lc(T<2>(t.c2.c1)));
+  return r;
+}
+#else
 BLS_FN fp12 fp12_sqr(const fp12& a) {
   fp6 t = fp6_mul(a.c0, a.c1);
   fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
@@ -339,6 +468,7 @@ BLS_FN fp12 fp12_sqr(const fp12& a) {
   fp6 c1 = fp6_add(t, t);
   return fp12_make(c0, c1);
 }
+#endif
 
 BLS_HD fp12 fp12_conj(const fp12& a) { return fp12_make(a.c0, fp6_neg(a.c1)); }
 
@@ -349,6 +479,43 @@ BLS_BIG fp12 fp12_inv(const fp12& a) {
 }
 
 // f * line, line = l0 + l1 v + l4 v w   (positions c0.c0, c0.c1, c1.c1) -- 13 Fp2 multiplications
+#if BLS_LAZY_014
+// A0 = f0 (l0 + l1 v) (reduced), A1 = f1 (l4 v) = (xi Q1, Q2, Q3) with Qk = f1.c(k-1 mod 3) l4 kept as raw products,
+// S = (f0 + f1)(l0 + (l1 + l4) v); c0 = A0 + v A1 = (A0.c0 + xi Q3, A0.c1 + xi Q1, A0.c2 + Q2), c1 = S - A0 - A1 with
+// S's five products folded straight into c1's combinations.  f, l: normalized, values <= 2p.
+BLS_FN fp12 fp12_mul_by_014(const fp12& f, const fp2& l0, const fp2& l1, const fp2& l4) {
+  fp6 b;  // f0 + f1 (values <= 4p, normalized)
+  b.c0 = fp2_make(fp_add_norm(f.c0.c0.c0, f.c1.c0.c0), fp_add_norm(f.c0.c0.c1, f.c1.c0.c1));
+  b.c1 = fp2_make(fp_add_norm(f.c0.c1.c0, f.c1.c1.c0), fp_add_norm(f.c0.c1.c1, f.c1.c1.c1));
+  b.c2 = fp2_make(fp_add_norm(f.c0.c2.c0, f.c1.c2.c0), fp_add_norm(f.c0.c2.c1, f.c1.c2.c1));
+  const fp2 Q1 = fp2_mul(f.c1.c2, l4), Q2 = fp2_mul(f.c1.c0, l4), Q3 = fp2_mul(f.c1.c1, l4);
+  const fp6 A0 = fp6_mul_by_01(f.c0, l0, l1);
+  fp12 r;
+  r.c0.c0 = fp2_make(fp_lc(T<1>(A0.c0.c0), T<1>(Q3.c0), T<-1>(Q3.c1)), fp_lc(T<1>(A0.c0.c1), T<1>(Q3.c0), T<1>(Q3.c1)));
+  r.c0.c1 = fp2_make(fp_lc(T<1>(A0.c1.c0), T<1>(Q1.c0), T<-1>(Q1.c1)), fp_lc(T<1>(A0.c1.c1), T<1>(Q1.c0), T<1>(Q1.c1)));
+  r.c0.c2 = fp2_make(fp_lc(T<1>(A0.c2.c0), T<1>(Q2.c0)), fp_lc(T<1>(A0.c2.c1), T<1>(Q2.c1)));
+  // S = b (l0 + m v), m = l1 + l4: R1 = b0 l0, R2 = b1 m, R3 = b2 m, R4 = (b0 + b1)(l0 + m), R5 = b2 l0;
+  // S = (R1 + xi R3, R4 - R1 - R2, R5 + R2)
+  const fp2 m = fp2_make(fp_add_norm(l1.c0, l4.c0), fp_add_norm(l1.c1, l4.c1));
+  const fp2 R1 = fp2_mul(b.c0, l0), R2 = fp2_mul(b.c1, m);
+  {
+    const fp2 R4 = fp2_mul(fp2_add_nr(b.c0, b.c1), fp2_add_nr(l0, m));
+    r.c1.c1 = fp2_make(fp_lc(T<1>(R4.c0), T<-1>(R1.c0), T<-1>(R2.c0), T<-1>(A0.c1.c0), T<-1>(Q2.c0)),
+                       fp_lc(T<1>(R4.c1), T<-1>(R1.c1), T<-1>(R2.c1), T<-1>(A0.c1.c1), T<-1>(Q2.c1)));
+  }
+  {
+    const fp2 R3 = fp2_mul(b.c2, m);
+    r.c1.c0 = fp2_make(fp_lc(T<1>(R1.c0), T<1>(R3.c0), T<-1>(R3.c1), T<-1>(A0.c0.c0), T<-1>(Q1.c0), T<1>(Q1.c1)),
+                       fp_lc(T<1>(R1.c1), T<1>(R3.c0), T<1>(R3.c1), T<-1>(A0.c0.c1), T<-1>(Q1.c0), T<-1>(Q1.c1)));
+  }
+  {
+    const fp2 R5 = fp2_mul(b.c2, l0);
+    r.c1.c2 = fp2_make(fp_lc(T<1>(R5.c0), T<1>(R2.c0), T<-1>(A0.c2.c0), T<-1>(Q3.c0)),
+                       fp_lc(T<1>(R5.c1), T<1>(R2.c1), T<-1>(A0.c2.c1), T<-1>(Q3.c1)));
+  }
+  return r;
+}
+#else
 BLS_FN fp12 fp12_mul_by_014(const fp12& f, const fp2& l0, const fp2& l1, const fp2& l4) {
   fp6 a0 = fp6_mul_by_01(f.c0, l0, l1);
   fp6 a1 = fp6_mul_by_1(f.c1, l4);
@@ -357,6 +524,7 @@ BLS_FN fp12 fp12_mul_by_014(const fp12& f, const fp2& l0, const fp2& l1, const f
   fp6 c0 = fp6_add(a0, fp6_mul_v(a1));
   return fp12_make(c0, c1);
 }
+#endif
 
 // Squaring in the cyclotomic subgroup (Granger-Scott, eprint 2009/565 section 3.2): f^(p^6+1) = 1 lets
 // f^2 be computed from three Fp4 squarings -- 9 Fp2 squarings (18 Fp products) instead of 36.

@@ -431,3 +431,50 @@ extern "C" int emu_hash_to_g2_split(const uint8_t* msg, uint8_t* out192) {
   g2a_to_be192(a, out192);
   return 1;
 }
+
+// fp_lc at the edges of its contract (raw 14-limb terms, normalized, values <= 2p): 7 positive and 8 negative unit
+// terms, and weighted terms 2, -3, 5, -4, 1
+extern "C" void emu_fp_lc_7p8n(const uint32_t* in, uint32_t* out14) {
+  fp x[15];
+  for (int k = 0; k < 15; k++)
+    for (int i = 0; i < BLS_NL; i++) x[k].l[i] = in[14 * k + i];
+  const fp r = fp_lc(T<1>(x[0]), T<1>(x[1]), T<1>(x[2]), T<1>(x[3]), T<1>(x[4]), T<1>(x[5]), T<1>(x[6]), T<-1>(x[7]),
+                     T<-1>(x[8]), T<-1>(x[9]), T<-1>(x[10]), T<-1>(x[11]), T<-1>(x[12]), T<-1>(x[13]), T<-1>(x[14]));
+  for (int i = 0; i < BLS_NL; i++) out14[i] = r.l[i];
+}
+extern "C" void emu_fp_lc_weighted(const uint32_t* in, uint32_t* out14) {
+  fp x[5];
+  for (int k = 0; k < 5; k++)
+    for (int i = 0; i < BLS_NL; i++) x[k].l[i] = in[14 * k + i];
+  const fp r = fp_lc(T<2>(x[0]), T<-3>(x[1]), T<5>(x[2]), T<-4>(x[3]), T<1>(x[4]));
+  for (int i = 0; i < BLS_NL; i++) out14[i] = r.l[i];
+}
+
+// k_pk_aggregate's schedule on the host: 64 strided lane sums of mixed additions, then the pairwise jac_add tree
+extern "C" int emu_g1_aggregate(const uint8_t* pks96, int n, uint8_t* out96) {
+  g1j acc[64];
+  for (int l = 0; l < 64; l++) acc[l] = jac_infinity<fp>();
+  for (int k = 0; k < n; k++) acc[k % 64] = jac_add_aff(acc[k % 64], load_g1(pks96 + 96 * k));
+  for (int s = 32; s >= 1; s >>= 1)
+    for (int l = 0; l < s; l++) acc[l] = jac_add(acc[l], acc[l + s]);
+  g1a r;
+  if (!jac_to_aff(acc[0], r)) return 0;
+  fp_to_be48(r.x, out96);
+  fp_to_be48(r.y, out96 + 48);
+  return 1;
+}
+
+// fp2_sqr at the edge of its operand contract: raw normalized limbs, values <= 4p (fp2_add_norm of two stored values);
+// the old fp_sub form underflowed for a1 - a0 > 2p
+extern "C" void emu_fp2_sqr_limbs(const uint32_t* in28, uint32_t* out28) {
+  fp2 a;
+  for (int i = 0; i < BLS_NL; i++) {
+    a.c0.l[i] = in28[i];
+    a.c1.l[i] = in28[14 + i];
+  }
+  const fp2 r = fp2_sqr(a);
+  for (int i = 0; i < BLS_NL; i++) {
+    out28[i] = r.c0.l[i];
+    out28[14 + i] = r.c1.l[i];
+  }
+}

@@ -411,3 +411,74 @@ def test_cooperative_g2_doubling_chain():
     for q in pts:
         assert L.emu_g2c_mul_zabs(g2b(q), o) == 1
         assert b2g2(o.raw) == bls.g2_mul(q, 0xD201000000010000)
+
+
+def _limbs14(v):
+    return [(v >> (28 * i)) & ((1 << 28) - 1) for i in range(13)] + [v >> (28 * 13)]
+
+
+def _val14(l):
+    return sum(x << (28 * i) for i, x in enumerate(l))
+
+
+def test_fp_lc_edges():
+    """fp_lc (fp.hpp): lazily reduced linear combinations at the edges of the contract -- terms of value 0, 1, p - 1,
+    p, 2p - 1, 2p and random values <= 2p, with the maximal weight 15 -- are the combination mod p, normalized, below
+    1.003 p."""
+    import random
+
+    L = lib()
+    L.emu_fp_lc_7p8n.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    L.emu_fp_lc_weighted.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    P = bls.P
+    edges = [0, 1, P - 1, P, 2 * P - 1, 2 * P, (1 << 28) - 1]
+    rnd = random.Random(11)
+    for trial in range(3000):
+        pick = lambda: rnd.choice(edges) if rnd.random() < 0.5 else rnd.randrange(0, 2 * P + 1)
+        if trial < 4:  # extreme sign patterns: all positives at 2p and negatives at 0, and the reverse
+            xs = [2 * P if (k < 7) == (trial % 2 == 0) else 0 for k in range(15)]
+        else:
+            xs = [pick() for _ in range(15)]
+        arr = (ctypes.c_uint32 * 210)(*sum((_limbs14(x) for x in xs), []))
+        out = (ctypes.c_uint32 * 14)()
+        L.emu_fp_lc_7p8n(arr, out)
+        v = _val14(list(out))
+        assert all(x < (1 << 28) for x in list(out)[:13]) and v < 1.003 * P
+        assert v % P == (sum(xs[:7]) - sum(xs[7:])) % P
+        ws = [2, -3, 5, -4, 1]
+        ys = xs[:5]
+        arr = (ctypes.c_uint32 * 70)(*sum((_limbs14(x) for x in ys), []))
+        L.emu_fp_lc_weighted(arr, out)
+        v = _val14(list(out))
+        assert all(x < (1 << 28) for x in list(out)[:13]) and v < 1.003 * P
+        assert v % P == sum(w * y for w, y in zip(ws, ys)) % P
+
+
+def test_fp2_sqr_operand_contract():
+    """fp2_sqr (tower.hpp) on normalized operands of value up to 4p -- the sums the lazy point formulas hand it
+    (F_add_sq / fp2_add_norm) -- including a1 - a0 > 2p, where the earlier a0 + 2p - a1 form underflowed: the Montgomery
+    square (a0 + a1 u)^2 R^-1, normalized, below 1.05 p."""
+    import random
+
+    L = lib()
+    L.emu_fp2_sqr_limbs.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    P = bls.P
+    Rinv = pow(1 << 392, -1, P)
+    rnd = random.Random(12)
+    edges = [0, 1, P - 1, P, 2 * P, 3 * P + 5, 4 * P - 1, 4 * P]
+    for trial in range(2000):
+        if trial < 64:
+            a0, a1 = edges[trial % 8], edges[trial // 8]
+        elif trial < 200:  # the underflow shape: a0 small, a1 near 4p
+            a0, a1 = rnd.randrange(0, P // 8), rnd.randrange(3 * P, 4 * P + 1)
+        else:
+            a0, a1 = rnd.randrange(0, 4 * P + 1), rnd.randrange(0, 4 * P + 1)
+        arr = (ctypes.c_uint32 * 28)(*(_limbs14(a0) + _limbs14(a1)))
+        out = (ctypes.c_uint32 * 28)()
+        L.emu_fp2_sqr_limbs(arr, out)
+        c0, c1 = _val14(list(out)[:14]), _val14(list(out)[14:])
+        for c in (list(out)[:13], list(out)[14:27]):
+            assert all(x < (1 << 28) for x in c)
+        assert c0 < 1.05 * P and c1 < 1.05 * P, (trial, c0 / P, c1 / P)
+        assert c0 % P == (a0 * a0 - a1 * a1) * Rinv % P, trial
+        assert c1 % P == 2 * a0 * a1 * Rinv % P, trial

@@ -250,3 +250,27 @@ def test_debug_scalar_word_mul():
             assert o2[2880 * k: 2880 * k + 192] == bls.g2_serialize(bls.g2_mul(Q, r))
     finally:
         ctx.close()
+
+
+def test_fp_lc_device_edges(ctx):
+    """fp_lc (fp.hpp) on the device (its MAD chain is inline assembly, so the host build does not cover it): terms at the
+    edges of the contract (0, 1, p - 1, p, 2p - 1, 2p, random <= 2p) -- the combination mod p, normalized, < 1.003 p."""
+    import random
+
+    from oracle import bls12_381 as bls
+
+    P = bls.P
+    rnd = random.Random(12)
+    edges = [0, 1, P - 1, P, 2 * P - 1, 2 * P]
+    cases = [[2 * P if (k < 7) == (t % 2 == 0) else 0 for k in range(15)] for t in range(2)]
+    cases += [[rnd.choice(edges) if rnd.random() < 0.5 else rnd.randrange(0, 2 * P + 1) for _ in range(15)]
+              for _ in range(4094)]
+    limbs = lambda v: [(v >> (28 * i)) & ((1 << 28) - 1) for i in range(13)] + [v >> (28 * 13)]
+    inp = b"".join(np.array(sum((limbs(x) for x in xs), []), np.uint32).tobytes() for xs in cases)
+    out, st = ctx.debug_op(11, inp, 15 * 56, 56)
+    assert (st == 0).all()
+    res = np.frombuffer(out, np.uint32).reshape(-1, 14)
+    for xs, r in zip(cases, res):
+        v = sum(int(x) << (28 * i) for i, x in enumerate(r))
+        assert (r[:13] < (1 << 28)).all() and v < 1.003 * P
+        assert v % P == (sum(xs[:7]) - sum(xs[7:])) % P
