@@ -47,6 +47,9 @@ static_assert(2 * WAVE <= BLS_FP2_LDS_LANES, "128-lane kernels (gt_wave.hpp, k_m
 #ifndef BLSGPU_WPE_HMAP
 #define BLSGPU_WPE_HMAP BLSGPU_WPE_HASH
 #endif
+#ifndef BLSGPU_WPE_GRP
+#define BLSGPU_WPE_GRP BLSGPU_WPE
+#endif
 
 // x, hidden from the optimizer: an SoA load whose lane index goes through this is recomputed where it is issued.
 // Inside a loop (the five additions of a [|z|] chain) the compiler otherwise hoists the point's 84 loop-invariant

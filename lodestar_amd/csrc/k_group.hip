@@ -57,7 +57,7 @@ __global__ __launch_bounds__(WAVE) void k_group_reduce(PipelineBuffers b, const 
 //   k_f_pairs   one 128-lane workgroup per pair (dst, src) of one tree level: f[dst] *= f[src] as a cooperative
 //               Fp12 product (gt_wave.hpp gtw_mul, ~5 us); the host plans the levels (runtime.cpp plan_f_tree)
 //   k_f_gather  lane per (group, word): F_g = the group's first chunk (one for a group without chunks)
-STAGE_KERNEL void k_f_runs(PipelineBuffers b, const uint32_t* runs, uint32_t n_runs) {
+STAGE_KERNEL_W(BLSGPU_WPE_GRP) void k_f_runs(PipelineBuffers b, const uint32_t* runs, uint32_t n_runs) {
   const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
   if (q >= n_runs) return;
   const uint32_t a = runs[2 * q], e = runs[2 * q + 1];
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(WAVE) void k_range_combine(const uint32_t* S_in, co
 // ---- lane-per-item forms of the fallback's reductions (many tiny ranges: one lane each) ----------------------
 
 // lane per range: S = sum of the range's included r_i sig_i (b.rsig), F = prod of its Miller chunks (b.f_chunk)
-STAGE_KERNEL void k_group_reduce_lane(PipelineBuffers b, const uint32_t* set_ranges, const uint32_t* f_ranges,
+STAGE_KERNEL_W(BLSGPU_WPE_GRP) void k_group_reduce_lane(PipelineBuffers b, const uint32_t* set_ranges, const uint32_t* f_ranges,
                                       uint32_t ng, uint32_t* S_out, uint32_t* F_out) {
   const uint32_t g = blockIdx.x * WAVE + threadIdx.x;
   if (g >= ng) return;
@@ -195,7 +195,7 @@ STAGE_KERNEL void k_group_reduce_lane(PipelineBuffers b, const uint32_t* set_ran
 }
 
 // lane per sub-group: S_out[r] = sum, F_out[r] = prod of entries ranges[2r] .. ranges[2r+1] (stride n_in)
-STAGE_KERNEL void k_range_combine_lane(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,
+STAGE_KERNEL_W(BLSGPU_WPE_GRP) void k_range_combine_lane(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,
                                        uint32_t n_out, uint32_t* S_out, uint32_t* F_out) {
   const uint32_t r = blockIdx.x * WAVE + threadIdx.x;
   if (r >= n_out) return;

@@ -25,13 +25,15 @@ def main(path, n, k=2):
         "pk_finish": (["k_pk_finish", "k_pk_affine"], ps["pk_finish"]["total"] * n),
         "sig_msm": (["k_msm_bucket", "k_msm_window", "k_msm_horner"],
                     ps["sig_msm"]["total"] * n + ops["per_group_fixed"]["sig_msm"] * groups),
-        "miller_lines": (["k_miller_lines"], ops["miller_lines_per_message"] * n),
-        "miller_acc": (["k_miller_acc"], ops["miller_acc_per_chunk"][str(k)] * n / k),
+        "miller_lines": (["k_miller_lines", "k_miller_lines2"], ops["miller_lines_per_message"] * n),
+        "miller_acc": (["k_miller_acc", "k_miller_acc2"], ops["miller_acc_per_chunk"][str(k)] * n / k),
     }
     rows = {}
     for r in csv.DictReader(open(path)):
         name = r["Name"].split("(")[0].replace("void ", "").split("<")[0]
         rows[name] = (int(r["Calls"]), float(r["AverageNs"]) * 1e-6)
+    if "k_miller_acc2" in rows:  # one item per chunk (two lanes per pairing): priced as k = 1
+        stage["miller_acc"] = (stage["miller_acc"][0], ops["miller_acc_per_chunk"]["1"] * n)
     calls = rows.get("k_sig_decode", (1, 0))[0]
     tot_ms = 0
     print(f"{'stage / kernel':28s} {'ms/launch':>10s} {'mults/launch':>13s} {'frac':>6s}")
