@@ -467,6 +467,7 @@ def main():
                     help="on an idle device, how long a slot waits while a burst of calls keeps arriving (runtime default)")
     ap.add_argument("--miller-k", type=int, default=0,
                     help="pairings per Miller accumulator (shared squarings); 0 = the runtime's choice by run size")
+    ap.add_argument("--f-run-max", type=int, default=0, help="F tree: longest lane-serial run (0 = runtime default)")
     ap.add_argument("--miller-lanes", type=int, default=0, help="lanes per pairing of one-item Miller chunks (0 = auto)")
     ap.add_argument("--sets", type=int, default=0, help="diagnostics: sets per call of C1/C2 (default the config's)")
     ap.add_argument("--serial", action="store_true",
@@ -511,6 +512,8 @@ def main():
         ctx.set_option("serial", 1)
     if args.miller_lanes:
         ctx.set_option("miller_lanes", args.miller_lanes)
+    if args.f_run_max:
+        ctx.set_option("f_run_max", args.f_run_max)
     work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev, sets=args.sets)
     expected = work.pop("expected", None)
     if expected is None:

@@ -1,10 +1,10 @@
 // A9 signature side of the random linear combination, S = sum_i r_i sig_i per range (a batch group, or one
 // job of the fallback), as a bucket multi-scalar multiplication (msm.hpp).  Three launches:
-//   k_msm_bucket   one 64-lane wave per slice (<= MSM_SLICE sets of one range), 128 buckets (window k = q / 8,
-//                  bucket e = q % 8).  Two counting passes over the slice's scalar words (in LDS) give every bucket
-//                  a compact list of its signed set indices (LDS, no atomics, so the order is deterministic); the
-//                  buckets are ranked by size and each lane sums a large and a small one (+-sig_i, mixed additions)
-//                  -> B[slice][q].  Lists keep the lanes busy on useful additions: ~len/8 per bucket.
+//   k_msm_bucket   one 128-lane workgroup per slice (<= MSM_SLICE sets of one range).  Lane t owns bucket
+//                  (window k = t / 8, bucket e = t % 8).  Two counting passes over the slice's scalar words (in
+//                  LDS) give every lane a compact list of its signed set indices (LDS, no atomics, so the order
+//                  is deterministic); the lane then sums +-sig_i with mixed additions -> B[slice][t].  Lists keep
+//                  the wave's lanes busy on useful additions: ~len/8 per lane instead of len masked ones.
 //   k_msm_window   eight lanes per (range, window): W = sum_e (2e + 1) sum_{slices of the range} B_e
 //   k_msm_horner   two 16-lane groups per range: S_a and lambda S_b (8-window Horner passes, cooperative
 //                  doublings), then S = their sum, written in the layout k_group_check reads
@@ -16,78 +16,46 @@
 
 #define MSM_LANES (MSM_WINDOWS * MSM_BUCKETS)
 
-// One 64-lane wave per slice, two buckets per lane paired by size: after the counting passes the 128 buckets are ranked
-// by their count and lane t sums bucket rank t then bucket rank 127 - t, so every lane carries about the mean of two
-// buckets (~2 len / 16 additions) instead of the wave waiting for its largest bucket (one bucket per lane over two
-// waves: ~1.4x the mean, measured as the bucket kernel's lockstep loss).  Lists and ranks in LDS, no atomics.
-#define MSM_BW 64
-__global__ __launch_bounds__(MSM_BW) __attribute__((amdgpu_waves_per_eu(BLSGPU_WPE_MSM, BLSGPU_WPE_MSM))) void k_msm_bucket(
+__global__ __launch_bounds__(MSM_LANES) __attribute__((amdgpu_waves_per_eu(BLSGPU_WPE_MSM, BLSGPU_WPE_MSM))) void k_msm_bucket(
     PipelineBuffers b, const uint32_t* slices, uint32_t n_slices, uint32_t* B) {
   __shared__ uint64_t sw[MSM_SLICE];
   __shared__ uint8_t act[MSM_SLICE];
   __shared__ uint16_t list[MSM_WINDOWS][MSM_SLICE];
   __shared__ uint16_t cnt[MSM_LANES];
-  __shared__ uint16_t off[MSM_LANES];
-  __shared__ uint8_t order[MSM_LANES];
   const uint32_t s = blockIdx.x, t = threadIdx.x;
   if (s >= n_slices) return;
   const uint32_t first = slices[2 * s], len = slices[2 * s + 1] - first;  // len <= MSM_SLICE (host)
-  for (uint32_t j = t; j < len; j += MSM_BW) {
+  for (uint32_t j = t; j < len; j += MSM_LANES) {
     const uint32_t i = first + j;
     act[j] = b.include[i] && !(b.flags[i] & SF_SIG_INF);
     sw[j] = b.scalars[i];
   }
   __syncthreads();
-  // counting: lane t counts buckets t and t + 64 (bucket q = window q / 8, digit bucket q % 8)
-#pragma unroll
-  for (uint32_t h = 0; h < 2; h++) {
-    const uint32_t q = t + h * MSM_BW;
-    const int k = (int)(q / MSM_BUCKETS);
-    const uint32_t e = q % MSM_BUCKETS;
-    uint32_t c = 0;
-    for (uint32_t j = 0; j < len; j++) {
-      bool neg;
-      c += (act[j] && msm_bucket(sw[j], k, neg) == e) ? 1u : 0u;
-    }
-    cnt[q] = (uint16_t)c;
+  const int k = (int)(t / MSM_BUCKETS);
+  const uint32_t e = t % MSM_BUCKETS;
+  uint32_t c = 0;
+  for (uint32_t j = 0; j < len; j++) {
+    bool neg;
+    c += (act[j] && msm_bucket(sw[j], k, neg) == e) ? 1u : 0u;
   }
+  cnt[t] = (uint16_t)c;
   __syncthreads();
-#pragma unroll
-  for (uint32_t h = 0; h < 2; h++) {
-    const uint32_t q = t + h * MSM_BW;
-    const int k = (int)(q / MSM_BUCKETS);
-    const uint32_t e = q % MSM_BUCKETS;
-    uint32_t o = 0;
-    for (uint32_t r = (uint32_t)k * MSM_BUCKETS; r < q; r++) o += cnt[r];
-    off[q] = (uint16_t)o;
-    for (uint32_t j = 0, p = o; j < len; j++) {
-      bool neg;
-      if (act[j] && msm_bucket(sw[j], k, neg) == e) list[k][p++] = (uint16_t)(j | (neg ? 0x8000u : 0u));
-    }
-    // rank: buckets with larger counts first (ties by index) -- a permutation of 0..127
-    uint32_t rank = 0;
-    const uint32_t cq = cnt[q];
-    for (uint32_t r = 0; r < MSM_LANES; r++) {
-      const uint32_t cr = cnt[r];
-      rank += (cr > cq || (cr == cq && r < q)) ? 1u : 0u;
-    }
-    order[rank] = (uint8_t)q;
+  uint32_t off = 0;
+  for (uint32_t q = (uint32_t)k * MSM_BUCKETS; q < t; q++) off += cnt[q];
+  for (uint32_t j = 0, p = off; j < len; j++) {
+    bool neg;
+    if (act[j] && msm_bucket(sw[j], k, neg) == e) list[k][p++] = (uint16_t)(j | (neg ? 0x8000u : 0u));
   }
-  __syncthreads();
+  // each lane reads back only the entries it wrote: no barrier
+  g2j acc = jac_infinity<fp2>();
 #pragma unroll 1
-  for (uint32_t h = 0; h < 2; h++) {
-    const uint32_t q = order[h ? MSM_LANES - 1 - t : t];
-    const uint32_t k = q / MSM_BUCKETS, o = off[q], c = cnt[q];
-    g2j acc = jac_infinity<fp2>();
-#pragma unroll 1
-    for (uint32_t x = 0; x < c; x++) {
-      const uint32_t v = list[k][o + x];
-      g2a P = ld_g2a(b.sig_aff, b.n, first + (v & 0x7fffu));
-      if (v & 0x8000u) P.y = fp2_neg(P.y);
-      acc = jac_add_aff(acc, P);
-    }
-    st_g2j(B, n_slices * MSM_LANES, s * MSM_LANES + q, acc);
+  for (uint32_t q = 0; q < c; q++) {
+    const uint32_t v = list[k][off + q];
+    g2a P = ld_g2a(b.sig_aff, b.n, first + (v & 0x7fffu));
+    if (v & 0x8000u) P.y = fp2_neg(P.y);
+    acc = jac_add_aff(acc, P);
   }
+  st_g2j(B, n_slices * MSM_LANES, s * MSM_LANES + t, acc);
 }
 
 // One lane per (range, window k, bucket e) -- the 8 lanes of a window are neighbours in one wave.  Range r covers
@@ -155,7 +123,7 @@ void launch_sig_msm(const PipelineBuffers& b, const uint32_t* slices, uint32_t n
                     uint32_t n_ranges, uint32_t* B, uint32_t* W, uint32_t* S, hipStream_t st) {
   if (!n_ranges) return;
   if (n_slices) {
-    hipLaunchKernelGGL(k_msm_bucket, dim3(n_slices), dim3(MSM_BW), 0, st, b, slices, n_slices, B);
+    hipLaunchKernelGGL(k_msm_bucket, dim3(n_slices), dim3(MSM_LANES), 0, st, b, slices, n_slices, B);
   }
   hipLaunchKernelGGL(k_msm_window, grid_for(n_ranges * MSM_LANES), dim3(WAVE), 0, st, range_slices, n_ranges, B,
                      n_slices, W);

@@ -198,9 +198,11 @@ struct Options {  // snapshot taken at the start of each call
   int64_t group_policy = 0;    // 0 = groups of >= group_sets sets; 1 = the reference pool's jobs / requests / chunks
   bool serial = false;  // diagnostics: every branch of a run on one stream (each kernel alone on the chip)
   int64_t miller_lanes = 0;  // lanes per pairing of the one-item-chunk Miller accumulation: 0 = by run size, 1, 2
+  int64_t f_run_max = 16;    // merged runs: longest lane-serial run of the F product tree before the cooperative pairs
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
-           group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes;
+           group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&
+           f_run_max == o.f_run_max;
   }
 };
 
@@ -541,7 +543,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   std::vector<uint32_t> ftree, f_level_end;
   uint32_t f_k = 1, f_max = 0;
   if (n_chunks > 16384)
-    while (n_chunks / f_k > 8192 && f_k < 16) f_k *= 2;
+    for (const uint32_t heads = opt.f_run_max > 16 ? 256u : 8192u;
+         n_chunks / f_k > heads && f_k < (uint32_t)opt.f_run_max;)
+      f_k *= 2;
   for (uint32_t g = 0; g < ng0; g++) f_max = std::max(f_max, g_chunks[2 * g + 1] - g_chunks[2 * g]);
   if (f_k > 1)
     for (uint32_t g = 0; g < ng0; g++)
@@ -1832,6 +1836,9 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "miller_lanes") {
     if (value < 0 || value > 2) return BLSGPU_ERR_ARGS;
     ctx->opt.miller_lanes = value;
+  } else if (k == "f_run_max") {
+    if (value < 1 || value > 1024 || (value & (value - 1))) return BLSGPU_ERR_ARGS;
+    ctx->opt.f_run_max = value;
   } else {
     return BLSGPU_ERR_ARGS;
   }
@@ -1874,6 +1881,7 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "pipeline_depth") *value = o.pipeline_depth;
   else if (k == "serial") *value = o.serial;
   else if (k == "miller_lanes") *value = o.miller_lanes;
+  else if (k == "f_run_max") *value = o.f_run_max;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }

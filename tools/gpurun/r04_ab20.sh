@@ -1,0 +1,13 @@
+# usage: bash tools/gpurun/r04_ab20.sh TAG REPS "lib1 lib2 ..." -- driver-command (20 steps, 5 warmup) C2 throughput of
+# library variants (default = in-tree build, else lodestar_amd/variants/<name>.so), interleaved over REPS rounds
+TAG=$1; REPS=$2; LIBS=$3
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+for r in $(seq 1 $REPS); do
+  for L in $LIBS; do
+    if [ "$L" = default ]; then P=""; else P=$GRAFT_REPO_ROOT/lodestar_amd/variants/$L.so; fi
+    BLSGPU_LIB=$P timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-parity \
+      > gpurun_out/${TAG}_${L}_$r.json 2> gpurun_out/${TAG}_${L}_$r.err || { echo "$L rep $r failed"; exit 1; }
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], sys.argv[3], d['value'], d.get('p50_batch_latency_ms'))" gpurun_out/${TAG}_${L}_$r.json $L $r
+  done
+done
