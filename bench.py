@@ -467,6 +467,9 @@ def main():
                     help="on an idle device, how long a slot waits while a burst of calls keeps arriving (runtime default)")
     ap.add_argument("--miller-k", type=int, default=0,
                     help="pairings per Miller accumulator (shared squarings); 0 = the runtime's choice by run size")
+    ap.add_argument("--lane-tail-min", type=int, default=-1,
+                    help="runs of >= this many sets use lane forms of the signature tails (-1 = runtime default, 0 never)")
+    ap.add_argument("--lane-tail-parts", type=int, default=-1, help="bit 0 Horner, bit 1 MillerLoop(-g1, S)")
     ap.add_argument("--f-run-max", type=int, default=0, help="F tree: longest lane-serial run (0 = runtime default)")
     ap.add_argument("--miller-lanes", type=int, default=0, help="lanes per pairing of one-item Miller chunks (0 = auto)")
     ap.add_argument("--sets", type=int, default=0, help="diagnostics: sets per call of C1/C2 (default the config's)")
@@ -514,6 +517,10 @@ def main():
         ctx.set_option("miller_lanes", args.miller_lanes)
     if args.f_run_max:
         ctx.set_option("f_run_max", args.f_run_max)
+    if args.lane_tail_parts >= 0:
+        ctx.set_option("lane_tail_parts", args.lane_tail_parts)
+    if args.lane_tail_min >= 0:
+        ctx.set_option("lane_tail_min", args.lane_tail_min)
     work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev, sets=args.sets)
     expected = work.pop("expected", None)
     if expected is None:

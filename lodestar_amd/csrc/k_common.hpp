@@ -138,6 +138,22 @@ __device__ __forceinline__ void st_fp12(uint32_t* p, uint32_t n, uint32_t i, con
   st_fp2(p, n, i, 8 * W_FP, f.c1.c1);
   st_fp2(p, n, i, 10 * W_FP, f.c1.c2);
 }
+// lane-pair exchange (lane ^ 1) of register values: __shfl_xor, no LDS
+BLS_INL fp fp_xlane(const fp& x) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = (uint32_t)__shfl_xor((int)x.l[i], 1);
+  return r;
+}
+BLS_INL fp2 fp2_xlane(const fp2& x) { return fp2_make(fp_xlane(x.c0), fp_xlane(x.c1)); }
+BLS_INL fp6 fp6_xlane(const fp6& x) { return fp6_make(fp2_xlane(x.c0), fp2_xlane(x.c1), fp2_xlane(x.c2)); }
+BLS_INL g2j g2j_xlane(const g2j& p) {
+  g2j r;
+  r.x = fp2_xlane(p.x);
+  r.y = fp2_xlane(p.y);
+  r.z = fp2_xlane(p.z);
+  return r;
+}
 __device__ __forceinline__ g1a ld_pktab(const uint32_t* tab, uint32_t idx) {
   const uint4* q = reinterpret_cast<const uint4*>(tab + (size_t)idx * W_PKTAB);
   uint32_t w[W_PKTAB];

@@ -120,6 +120,20 @@ __global__ __launch_bounds__(GTW_MILLER_LANES) void k_group_sig_miller(const uin
   for (uint32_t w = t; w < W_FP12; w += GTW_MILLER_LANES) G_out[(size_t)w * ng + g] = sh.G[gtw_lds_word(w)];
 }
 
+// The same G = MillerLoop(-g1, S) on one lane per group (pairing.hpp miller_loop: conj(f), the layout above) for
+// merged runs, where a three-wave cooperative workgroup waits for three free SIMDs of one CU (~20 ms per launch in the
+// driver's trace, on the run's critical path) while single waves take any free SIMD.
+STAGE_KERNEL_W(BLSGPU_WPE_GRP) void k_group_sig_miller_lane(const uint32_t* S_in, uint32_t ng, uint32_t* G_out) {
+  const uint32_t g = blockIdx.x * WAVE + threadIdx.x;
+  if (g >= ng) return;
+  g2a Sa;
+  g1a P;
+  P.x = G1_GEN_X;
+  P.y = G1_NEG_GEN_Y;
+  const fp12 G = jac_to_aff(ld_g2j(S_in, ng, g), Sa) ? miller_loop(P, Sa) : fp12_one();
+  st_fp12(G_out, ng, g, G);
+}
+
 // MILLER: G_in is null, the kernel runs MillerLoop(-g1, S) itself (three waves, gtw_miller_loop); otherwise two
 template <bool MILLER>
 __global__ __launch_bounds__(MILLER ? GTW_MILLER_LANES : GTW_LANES) void k_group_check(
@@ -251,8 +265,10 @@ void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8
     hipLaunchKernelGGL(k_group_check<true>, dim3(n), dim3(GTW_MILLER_LANES),
                        exclusive ? exclusive_cu_lds<k_group_check<true>>() : 0, s, S, F, ng, G, sel, ok);
 }
-void launch_group_sig_miller(const uint32_t* S, uint32_t ng, uint32_t* G, hipStream_t s, bool exclusive) {
-  if (ng)
+void launch_group_sig_miller(const uint32_t* S, uint32_t ng, uint32_t* G, hipStream_t s, bool exclusive, bool lane) {
+  if (ng && lane)
+    hipLaunchKernelGGL(k_group_sig_miller_lane, grid_for(ng), dim3(WAVE), 0, s, S, ng, G);
+  else if (ng)
     hipLaunchKernelGGL(k_group_sig_miller, dim3(ng), dim3(GTW_MILLER_LANES),
                        exclusive ? exclusive_cu_lds<k_group_sig_miller>() : 0,
                        s, S, ng, G);

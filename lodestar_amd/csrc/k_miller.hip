@@ -12,15 +12,6 @@
 #include "k_common.hpp"
 #include "gt_wave.hpp"
 
-// lane-pair exchange (lane ^ 1) of register values: __shfl_xor, no LDS
-BLS_INL fp fp_xlane(const fp& x) {
-  fp r;
-#pragma unroll
-  for (int i = 0; i < BLS_NL; i++) r.l[i] = (uint32_t)__shfl_xor((int)x.l[i], 1);
-  return r;
-}
-BLS_INL fp2 fp2_xlane(const fp2& x) { return fp2_make(fp_xlane(x.c0), fp_xlane(x.c1)); }
-BLS_INL fp6 fp6_xlane(const fp6& x) { return fp6_make(fp2_xlane(x.c0), fp2_xlane(x.c1), fp2_xlane(x.c2)); }
 BLS_INL fp fp_add_n(const fp& a, const fp& b) { return fp_add_norm(a, b); }
 
 STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_miller_lines(PipelineBuffers b) {

@@ -117,16 +117,33 @@ __global__ __launch_bounds__(MSM_H_LANES) void k_msm_horner(const uint32_t* W, u
   if (tg == 0 && on && !part) st_g2j(S, n_ranges, r, g2c_ld_point(g));
 }
 
+// The same two Horner passes on two LANES per range (lane 2r: S_a, lane 2r + 1: lambda S_b, then lane 2r adds its
+// partner's result through a lane exchange) -- for merged runs, where the chip is full of one-wave-per-SIMD stage
+// kernels: a 128-lane cooperative workgroup needs two free SIMDs of one CU at once and waited ~16 ms for them in the
+// driver's trace (the signature branch was the run's critical path); single waves take any free SIMD.
+STAGE_KERNEL void k_msm_horner_lane(const uint32_t* W, uint32_t n_ranges, uint32_t* S) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  const uint32_t r = q >> 1, part = q & 1;
+  if (r >= n_ranges) return;  // both lanes of a pair leave together (WAVE is even)
+  const uint32_t nw = n_ranges * MSM_WINDOWS;
+  const g2j h = msm_horner_half([&](int k) { return ld_g2j(W, nw, r * MSM_WINDOWS + (uint32_t)k); }, (int)part);
+  const g2j o = g2j_xlane(h);
+  if (!part) st_g2j(S, n_ranges, r, jac_add(h, o));
+}
+
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
 void launch_sig_msm(const PipelineBuffers& b, const uint32_t* slices, uint32_t n_slices, const uint32_t* range_slices,
-                    uint32_t n_ranges, uint32_t* B, uint32_t* W, uint32_t* S, hipStream_t st) {
+                    uint32_t n_ranges, uint32_t* B, uint32_t* W, uint32_t* S, hipStream_t st, bool lane_tail) {
   if (!n_ranges) return;
   if (n_slices) {
     hipLaunchKernelGGL(k_msm_bucket, dim3(n_slices), dim3(MSM_LANES), 0, st, b, slices, n_slices, B);
   }
   hipLaunchKernelGGL(k_msm_window, grid_for(n_ranges * MSM_LANES), dim3(WAVE), 0, st, range_slices, n_ranges, B,
                      n_slices, W);
-  hipLaunchKernelGGL(k_msm_horner, dim3((n_ranges + MSM_H_RANGES - 1) / MSM_H_RANGES), dim3(MSM_H_LANES), 0, st, W,
-                     n_ranges, S);
+  if (lane_tail)
+    hipLaunchKernelGGL(k_msm_horner_lane, grid_for(2 * n_ranges), dim3(WAVE), 0, st, W, n_ranges, S);
+  else
+    hipLaunchKernelGGL(k_msm_horner, dim3((n_ranges + MSM_H_RANGES - 1) / MSM_H_RANGES), dim3(MSM_H_LANES), 0, st, W,
+                       n_ranges, S);
 }

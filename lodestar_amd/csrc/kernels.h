@@ -107,8 +107,9 @@ void launch_sig_scale(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s, 
 #endif
 #define MSM_BUCKET_WORDS (128 * W_G2J)
 #define MSM_WINDOW_WORDS (16 * W_G2J)
+// lane_tail: the Horner passes on two lanes per range instead of cooperative 16-lane groups (merged runs)
 void launch_sig_msm(const PipelineBuffers& b, const uint32_t* slices, uint32_t n_slices, const uint32_t* range_slices,
-                    uint32_t n_ranges, uint32_t* B, uint32_t* W, uint32_t* S, hipStream_t s);
+                    uint32_t n_ranges, uint32_t* B, uint32_t* W, uint32_t* S, hipStream_t s, bool lane_tail = false);
 // per-job error status and the per-set include mask of the batch equation
 void launch_job_mask(const PipelineBuffers& b, hipStream_t s);
 // P_u = sum over the unit's included sets of r_i pk_i (affine)
@@ -147,7 +148,9 @@ void launch_group_tree(const PipelineBuffers& b, const uint32_t* f_ranges, uint3
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t n_groups, uint8_t* ok, hipStream_t s,
                         const uint32_t* sel = nullptr, uint32_t n_sel = 0, const uint32_t* G = nullptr,
                         bool exclusive = false);
-void launch_group_sig_miller(const uint32_t* S, uint32_t n_groups, uint32_t* G, hipStream_t s, bool exclusive = false);
+// lane: one lane per group (pairing.hpp miller_loop) instead of a three-wave cooperative workgroup (merged runs)
+void launch_group_sig_miller(const uint32_t* S, uint32_t n_groups, uint32_t* G, hipStream_t s, bool exclusive = false,
+                             bool lane = false);
 // lane-per-item forms (one lane per range / sub-group) for the fallback's many tiny ranges
 void launch_group_reduce_lane(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
                               uint32_t n_groups, uint32_t* S, uint32_t* F, hipStream_t s);

@@ -199,10 +199,14 @@ struct Options {  // snapshot taken at the start of each call
   bool serial = false;  // diagnostics: every branch of a run on one stream (each kernel alone on the chip)
   int64_t miller_lanes = 0;  // lanes per pairing of the one-item-chunk Miller accumulation: 0 = by run size, 1, 2
   int64_t f_run_max = 16;    // merged runs: longest lane-serial run of the F product tree before the cooperative pairs
+  int64_t lane_tail_min = 0;  // runs of >= this many sets take the lane forms of the Horner passes and the groups'
+                                  // MillerLoop(-g1, S) (0 = never)
+  int64_t lane_tail_parts = 3;    // bit 0: Horner passes, bit 1: MillerLoop(-g1, S)
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
            group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&
-           f_run_max == o.f_run_max;
+           f_run_max == o.f_run_max && lane_tail_min == o.lane_tail_min &&
+           lane_tail_parts == o.lane_tail_parts;
   }
 };
 
@@ -727,6 +731,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // each branch has its own stream shared by every run.
   const bool prof = opt.profile;
   const bool spec = BLSGPU_STREAM_PAIRS && coop && sl.alone && !opt.serial;  // speculative MSM (below)
+  // Large (merged) runs meet a chip full of one-wave-per-SIMD stage kernels: the signature branch's cooperative tails
+  // (Horner passes, MillerLoop(-g1, S)) waited for free SIMD groups there, so they run on single lanes
+  const bool lane_tail = opt.lane_tail_min > 0 && n >= (uint32_t)opt.lane_tail_min;
   // A small run that found the device idle puts its pubkey branch on the other pair's (idle) signature stream, beside
   // its own signature decode and subgroup checks instead of in front of them: the signature branch was a small
   // call's critical path (C1 serial trace: 7.25 ms vs the message branch's 6.15).
@@ -814,11 +821,13 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     if (spec)
       HIPCHK(hipStreamWaitEvent(s, sl.join_msm, 0));
     else
-      launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s);
+      launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s,
+                     lane_tail && (opt.lane_tail_parts & 1));
     end(4, s);
     // MillerLoop(-g1, S_g) of every group now, while the message branch still runs
     beg(kStages + 1, s);
-    launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, s, BLSGPU_EXCLUSIVE_SMALL && coop);
+    launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, s, BLSGPU_EXCLUSIVE_SMALL && coop,
+                            lane_tail && (opt.lane_tail_parts & 2));
     end(kStages + 1, s);
     HIPCHK(hipEventRecord(sl.join_gsm, s));
     HIPCHK(hipStreamWaitEvent(stl, sl.join_gsm, 0));
@@ -1836,6 +1845,12 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "miller_lanes") {
     if (value < 0 || value > 2) return BLSGPU_ERR_ARGS;
     ctx->opt.miller_lanes = value;
+  } else if (k == "lane_tail_parts") {
+    if (value < 0 || value > 3) return BLSGPU_ERR_ARGS;
+    ctx->opt.lane_tail_parts = value;
+  } else if (k == "lane_tail_min") {
+    if (value < 0) return BLSGPU_ERR_ARGS;
+    ctx->opt.lane_tail_min = value;
   } else if (k == "f_run_max") {
     if (value < 1 || value > 1024 || (value & (value - 1))) return BLSGPU_ERR_ARGS;
     ctx->opt.f_run_max = value;
@@ -1882,6 +1897,8 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "serial") *value = o.serial;
   else if (k == "miller_lanes") *value = o.miller_lanes;
   else if (k == "f_run_max") *value = o.f_run_max;
+  else if (k == "lane_tail_min") *value = o.lane_tail_min;
+  else if (k == "lane_tail_parts") *value = o.lane_tail_parts;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }

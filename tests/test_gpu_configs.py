@@ -137,3 +137,16 @@ def test_pool_policy_split_calls_vs_oracle(ctx):
     clean = dict(call, sigs=sigs, sig_len=[96] * n, msgs=b"".join(msgs), sig_stride=96)
     got, st = compare(ctx, clean, None, policy=1)
     assert (np.delete(got, 4) == 1).all() and st.batch_retries == 0
+
+
+def test_c5_lane_tails_vs_oracle(ctx):
+    """The lane forms of the signature tails (two-lane Horner passes, one-lane MillerLoop(-g1, S) per group; merged
+    runs by default) forced on every run of the C5 workload: the same results as the oracle job for job."""
+    w, n, desc, _ = bench.build_workload(ctx, "C5", 0, signer=oracle_sign)
+    table = bench.oracle_table(w)
+    ctx.set_option("lane_tail_min", 1)
+    try:
+        got, st = compare(ctx, call_of(w), table)
+    finally:
+        ctx.set_option("lane_tail_min", 0)
+    assert np.array_equal(got, w["expected"])
