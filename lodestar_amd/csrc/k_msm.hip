@@ -62,15 +62,31 @@ __global__ __launch_bounds__(MSM_LANES) __attribute__((amdgpu_waves_per_eu(BLSGP
 // slices [range_slices[r], range_slices[r + 1]); the lane sums its bucket over them (4 slices of a 16k call: 3
 // additions), forms (2e + 1) B_e and the window's lanes sum their terms through LDS in a 3-level tree
 // (msm_odd_multiple / msm_window_sum_tree): W_k in 3 + 6 additions + 3 doublings of depth instead of 3 x 8 + 18.
+// One level of a pairwise tree over a range's slices (latency-bound runs with many short slices): lane per (range,
+// pair j, bucket) adds slice s0 + (2j + 1) stride into slice s0 + 2j stride in place, so after ceil(log2(slices))
+// levels the first slice of every range holds the range's bucket sums -- the window lanes' serial sum over 32 slices
+// becomes 5 additions deep.
+STAGE_KERNEL void k_msm_slice_pairs(const uint32_t* range_slices, uint32_t n_ranges, uint32_t* B, uint32_t n_slices,
+                                    uint32_t stride, uint32_t max_pairs) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  const uint32_t tb = q % MSM_LANES, rest = q / MSM_LANES, j = rest % max_pairs, r = rest / max_pairs;
+  if (r >= n_ranges) return;
+  const uint32_t s0 = range_slices[r], s1 = range_slices[r + 1], a = s0 + 2 * j * stride, c = a + stride;
+  if (c >= s1) return;
+  const uint32_t nb = n_slices * MSM_LANES;
+  st_g2j(B, nb, a * MSM_LANES + tb, jac_add(ld_g2j(B, nb, a * MSM_LANES + tb), ld_g2j(B, nb, c * MSM_LANES + tb)));
+}
+
 STAGE_KERNEL void k_msm_window(const uint32_t* range_slices, uint32_t n_ranges, const uint32_t* B, uint32_t n_slices,
-                               uint32_t* W) {
+                               uint32_t* W, bool presummed) {
   __shared__ uint32_t xch[W_G2J * WAVE];
   const uint32_t t = threadIdx.x, q = blockIdx.x * WAVE + t;
   const bool on = q < n_ranges * MSM_LANES;
   const uint32_t r = q / MSM_LANES, tb = q % MSM_LANES, e = tb % MSM_BUCKETS;
   g2j T = jac_infinity<fp2>();
   if (on) {
-    const uint32_t s0 = range_slices[r], s1 = range_slices[r + 1], nb = n_slices * MSM_LANES;
+    const uint32_t s0 = range_slices[r], s1 = presummed ? std::min(range_slices[r + 1], s0 + 1) : range_slices[r + 1],
+                   nb = n_slices * MSM_LANES;
     if (s0 < s1) T = ld_g2j(B, nb, s0 * MSM_LANES + tb);
 #pragma unroll 1
     for (uint32_t s = s0 + 1; s < s1; s++) T = jac_add(T, ld_g2j(B, nb, s * MSM_LANES + tb));
@@ -134,13 +150,21 @@ STAGE_KERNEL void k_msm_horner_lane(const uint32_t* W, uint32_t n_ranges, uint32
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
 void launch_sig_msm(const PipelineBuffers& b, const uint32_t* slices, uint32_t n_slices, const uint32_t* range_slices,
-                    uint32_t n_ranges, uint32_t* B, uint32_t* W, uint32_t* S, hipStream_t st, bool lane_tail) {
+                    uint32_t n_ranges, uint32_t* B, uint32_t* W, uint32_t* S, hipStream_t st, bool lane_tail,
+                    uint32_t tree_slices) {
   if (!n_ranges) return;
   if (n_slices) {
     hipLaunchKernelGGL(k_msm_bucket, dim3(n_slices), dim3(MSM_LANES), 0, st, b, slices, n_slices, B);
   }
+  const bool tree = n_slices && tree_slices > 2;
+  if (tree)
+    for (uint32_t stride = 1; stride < tree_slices; stride *= 2) {
+      const uint32_t max_pairs = (tree_slices + 2 * stride - 1) / (2 * stride);
+      hipLaunchKernelGGL(k_msm_slice_pairs, grid_for(n_ranges * max_pairs * MSM_LANES), dim3(WAVE), 0, st,
+                         range_slices, n_ranges, B, n_slices, stride, max_pairs);
+    }
   hipLaunchKernelGGL(k_msm_window, grid_for(n_ranges * MSM_LANES), dim3(WAVE), 0, st, range_slices, n_ranges, B,
-                     n_slices, W);
+                     n_slices, W, tree);
   if (lane_tail)
     hipLaunchKernelGGL(k_msm_horner_lane, grid_for(2 * n_ranges), dim3(WAVE), 0, st, W, n_ranges, S);
   else

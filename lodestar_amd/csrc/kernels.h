@@ -108,8 +108,11 @@ void launch_sig_scale(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s, 
 #define MSM_BUCKET_WORDS (128 * W_G2J)
 #define MSM_WINDOW_WORDS (16 * W_G2J)
 // lane_tail: the Horner passes on two lanes per range instead of cooperative 16-lane groups (merged runs)
+// tree_slices: the most slices of any range; > 2 sums each range's slices by a pairwise tree of launches before the
+// window pass (latency-bound runs with short slices), else the window lanes sum them serially
 void launch_sig_msm(const PipelineBuffers& b, const uint32_t* slices, uint32_t n_slices, const uint32_t* range_slices,
-                    uint32_t n_ranges, uint32_t* B, uint32_t* W, uint32_t* S, hipStream_t s, bool lane_tail = false);
+                    uint32_t n_ranges, uint32_t* B, uint32_t* W, uint32_t* S, hipStream_t s, bool lane_tail = false,
+                    uint32_t tree_slices = 0);
 // per-job error status and the per-set include mask of the batch equation
 void launch_job_mask(const PipelineBuffers& b, hipStream_t s);
 // P_u = sum over the unit's included sets of r_i pk_i (affine)

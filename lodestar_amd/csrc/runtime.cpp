@@ -202,11 +202,14 @@ struct Options {  // snapshot taken at the start of each call
   int64_t lane_tail_min = 0;  // runs of >= this many sets take the lane forms of the Horner passes and the groups'
                                   // MillerLoop(-g1, S) (0 = never)
   int64_t lane_tail_parts = 3;    // bit 0: Horner passes, bit 1: MillerLoop(-g1, S)
+  int64_t msm_slice_mid = 32;     // MSM slice length of runs of 1k-32k sets
+  int64_t msm_tree = 1;           // those runs sum each range's slices by a pairwise tree
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
            group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&
            f_run_max == o.f_run_max && lane_tail_min == o.lane_tail_min &&
-           lane_tail_parts == o.lane_tail_parts;
+           lane_tail_parts == o.lane_tail_parts &&
+           msm_slice_mid == o.msm_slice_mid && msm_tree == o.msm_tree;
   }
 };
 
@@ -531,15 +534,21 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // 3.55 -> 2.80 ms; merged runs keep full slices (fewer bucket sums to combine: 100-step C2 3.13M vs 3.01M).
   // Small runs (<= 1024 sets) take 32-set slices: a bucket lane's chain of mixed additions is ~len / 8 plus its
   // spread (128 sets: ~25 additions on the slowest lane, 1.26 ms), the window lanes add the few slices up.
+  // Up to 32k sets the slice length is opt.msm_slice_mid (default 32: a 16k call's bucket pass is 512 workgroups, every
+  // SIMD a wave, ~4 additions per lane) and each range's slices are summed by a pairwise tree of launches
+  // (launch_sig_msm tree_slices) instead of the window lanes' serial chain.
   constexpr uint32_t kMsmHalfSliceMaxSets = 32768, kMsmSmallSliceMaxSets = 1024;
   const uint32_t slice_len = n <= kMsmSmallSliceMaxSets  ? 32
-                             : n <= kMsmHalfSliceMaxSets ? MSM_SLICE / 2
+                             : n <= kMsmHalfSliceMaxSets ? (uint32_t)opt.msm_slice_mid
                                                          : MSM_SLICE;
   std::vector<uint32_t> slices, range_slices{0};
+  uint32_t msm_tree = 0;  // most slices of a range, when the tree sums them
   for (uint32_t g = 0; g < ng0; g++)
     add_slices(slices, range_slices, job_sets(group_jobs[g].first).first, job_sets(group_jobs[g].second - 1).second,
                slice_len);
   const uint32_t n_slices = (uint32_t)(slices.size() / 2);
+  if (n > kMsmSmallSliceMaxSets && n <= kMsmHalfSliceMaxSets && opt.msm_tree)
+    for (uint32_t g = 0; g < ng0; g++) msm_tree = std::max(msm_tree, range_slices[g + 1] - range_slices[g]);
   // F_g = prod of the group's Miller chunks as a product tree (launch_group_tree): with more than 16384 chunks (merged
   // runs), runs of f_k consecutive chunks first (lane-serial: a 128-lane cooperative product costs ~6x the lane
   // time) down to <= 8192 heads, then pair levels of stride f_k, 2 f_k, ... (one cooperative workgroup per pair);
@@ -796,7 +805,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     if (spec) {
       HIPCHK(hipStreamWaitEvent(smsm, sl.join_dec, 0));
       launch_spec_mask(pb, n, pbm.include, smsm);
-      launch_sig_msm(pbm, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, smsm);
+      launch_sig_msm(pbm, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, smsm, false,
+                     msm_tree);
       HIPCHK(hipEventRecord(sl.join_msm, smsm));
     }
     HIPCHK(hipStreamWaitEvent(s, sl.join_pk, 0));
@@ -822,7 +832,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       HIPCHK(hipStreamWaitEvent(s, sl.join_msm, 0));
     else
       launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s,
-                     lane_tail && (opt.lane_tail_parts & 1));
+                     lane_tail && (opt.lane_tail_parts & 1), msm_tree);
     end(4, s);
     // MillerLoop(-g1, S_g) of every group now, while the message branch still runs
     beg(kStages + 1, s);
@@ -1845,6 +1855,11 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "miller_lanes") {
     if (value < 0 || value > 2) return BLSGPU_ERR_ARGS;
     ctx->opt.miller_lanes = value;
+  } else if (k == "msm_slice_mid") {
+    if (value < 8 || value > MSM_SLICE) return BLSGPU_ERR_ARGS;
+    ctx->opt.msm_slice_mid = value;
+  } else if (k == "msm_tree") {
+    ctx->opt.msm_tree = value != 0;
   } else if (k == "lane_tail_parts") {
     if (value < 0 || value > 3) return BLSGPU_ERR_ARGS;
     ctx->opt.lane_tail_parts = value;
@@ -1899,6 +1914,8 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "f_run_max") *value = o.f_run_max;
   else if (k == "lane_tail_min") *value = o.lane_tail_min;
   else if (k == "lane_tail_parts") *value = o.lane_tail_parts;
+  else if (k == "msm_slice_mid") *value = o.msm_slice_mid;
+  else if (k == "msm_tree") *value = o.msm_tree;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }
