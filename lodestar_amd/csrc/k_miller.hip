@@ -151,30 +151,20 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc(PipelineBuffers b) {
 // no LDS).  Per step each lane does one Fp6 product of the complex squaring (lane 0: t = c0 c1, lane 1:
 // s = (c0 + c1)(c0 + v c1); then c1' = 2t, c0' = s - t - v t) and one half of the sparse line product
 // (c0' = c0 L01 + v (c1 l4 v), c1' = c1 L01 + c0 (l4 v)): 14 Fp2 products per lane per step against 25 on one lane, so
-// a pairing takes ~0.56 of the lane-per-pairing time (12% more work in all).  One item per chunk.
+// a pairing takes ~0.56 of the lane-per-pairing time (12% more work in all).  A chunk of K items shares the squaring
+// (one per step, split as above) and takes each item's sparse product on the two halves: f's 168 words never sit on
+// one lane, so the kernel runs without spills (the one-lane chunk form spilled ~100 KB of scratch traffic per pairing).
 template <bool UNITS>
 STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc2(PipelineBuffers b) {
   const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
   const uint32_t c = q >> 1, h = q & 1;  // both lanes of a pair see the same c (WAVE is even)
   if (c >= b.n_chunks) return;           // whole pairs leave together: the exchanges below stay within live pairs
-  const uint32_t i = b.chunk_items[b.chunk_first[c]];
-  uint32_t m;
-  bool active;
-  if (UNITS) {
-    m = b.unit_msg[i];
-    active = b.unit_ok[i] != 0;
-  } else {
-    m = b.msg_idx[i];
-    active = b.include[i] != 0;
-  }
-  active = active && !(b.mflags[m] & MF_H_INF);  // the same on both lanes of the pair
-  g1a P;
-  if (active) P = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
+  const uint32_t k0 = b.chunk_first[c], k1 = b.chunk_first[c + 1];
   fp6 mine = h ? fp6_zero() : fp6_one();
   int bit = 62;
   bool add_next = false;
 #pragma unroll 1
-  for (int s = 0; s < MILLER_STEPS && active; s++) {
+  for (int s = 0; s < MILLER_STEPS; s++) {
     if (!add_next && s != 0) {
       const fp6 other = fp6_xlane(mine);
       const fp6 a0 = h ? other : mine, a1 = h ? mine : other;
@@ -209,19 +199,34 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc2(PipelineBuffers b) {
       mine = fp6_xlane(r);  // lane 0 computed c1', lane 1 c0': swap back
     }
     const uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
-    const fp2 l0 = ld_fp2(o, b.nm, m, 0);
-    const fp2 l1 = fp2_mul_fp(ld_fp2(o, b.nm, m, 2 * W_FP), P.x);
-    const fp2 l4 = fp2_mul_fp(ld_fp2(o, b.nm, m, 4 * W_FP), P.y);
-    // lane 0: c0' = c0 (l0 + l1 v) + v (c1 (l4 v)); lane 1: c1' = c1 (l0 + l1 v) + c0 (l4 v)
-    const fp6 other = fp6_xlane(mine);
-    const fp6 A = fp6_mul_by_01(mine, l0, l1);  // own half times (l0 + l1 v)
-    const fp6 Z = fp6_mul_by_1(other, l4);
-    const fp6 Zv = h ? Z : fp6_mul_v(Z);
-    fp6 r;
-    r.c0 = fp2_make(fp_lc(T<1>(A.c0.c0), T<1>(Zv.c0.c0)), fp_lc(T<1>(A.c0.c1), T<1>(Zv.c0.c1)));
-    r.c1 = fp2_make(fp_lc(T<1>(A.c1.c0), T<1>(Zv.c1.c0)), fp_lc(T<1>(A.c1.c1), T<1>(Zv.c1.c1)));
-    r.c2 = fp2_make(fp_lc(T<1>(A.c2.c0), T<1>(Zv.c2.c0)), fp_lc(T<1>(A.c2.c1), T<1>(Zv.c2.c1)));
-    mine = r;
+#pragma unroll 1
+    for (uint32_t k = k0; k < k1; k++) {
+      const uint32_t i = b.chunk_items[k];
+      uint32_t m;
+      bool active;
+      if (UNITS) {
+        m = b.unit_msg[i];
+        active = b.unit_ok[i] != 0;
+      } else {
+        m = b.msg_idx[i];
+        active = b.include[i] != 0;
+      }
+      if (!active || (b.mflags[m] & MF_H_INF)) continue;  // the same on both lanes of the pair
+      const g1a P = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
+      const fp2 l0 = ld_fp2(o, b.nm, m, 0);
+      const fp2 l1 = fp2_mul_fp(ld_fp2(o, b.nm, m, 2 * W_FP), P.x);
+      const fp2 l4 = fp2_mul_fp(ld_fp2(o, b.nm, m, 4 * W_FP), P.y);
+      // lane 0: c0' = c0 (l0 + l1 v) + v (c1 (l4 v)); lane 1: c1' = c1 (l0 + l1 v) + c0 (l4 v)
+      const fp6 other = fp6_xlane(mine);
+      const fp6 A = fp6_mul_by_01(mine, l0, l1);  // own half times (l0 + l1 v)
+      const fp6 Z = fp6_mul_by_1(other, l4);
+      const fp6 Zv = h ? Z : fp6_mul_v(Z);
+      fp6 r;
+      r.c0 = fp2_make(fp_lc(T<1>(A.c0.c0), T<1>(Zv.c0.c0)), fp_lc(T<1>(A.c0.c1), T<1>(Zv.c0.c1)));
+      r.c1 = fp2_make(fp_lc(T<1>(A.c1.c0), T<1>(Zv.c1.c0)), fp_lc(T<1>(A.c1.c1), T<1>(Zv.c1.c1)));
+      r.c2 = fp2_make(fp_lc(T<1>(A.c2.c0), T<1>(Zv.c2.c0)), fp_lc(T<1>(A.c2.c1), T<1>(Zv.c2.c1)));
+      mine = r;
+    }
     if (!add_next) {
       add_next = (BLS_Z_ABS >> bit) & 1ull;
       bit--;

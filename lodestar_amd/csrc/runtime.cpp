@@ -203,13 +203,15 @@ struct Options {  // snapshot taken at the start of each call
                                   // MillerLoop(-g1, S) (0 = never)
   int64_t lane_tail_parts = 3;    // bit 0: Horner passes, bit 1: MillerLoop(-g1, S)
   int64_t msm_slice_mid = 32;     // MSM slice length of runs of 1k-32k sets
+  int64_t lines_lanes = 1;        // lanes per message of the Miller lines (1, 2)
   int64_t msm_tree = 1;           // those runs sum each range's slices by a pairwise tree
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
            group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&
            f_run_max == o.f_run_max && lane_tail_min == o.lane_tail_min &&
            lane_tail_parts == o.lane_tail_parts &&
-           msm_slice_mid == o.msm_slice_mid && msm_tree == o.msm_tree;
+           msm_slice_mid == o.msm_slice_mid && msm_tree == o.msm_tree &&
+           lines_lanes == o.lines_lanes;
   }
 };
 
@@ -241,8 +243,9 @@ inline uint32_t miller_k_auto(uint32_t n_items) {
 // The Miller accumulation of a run's chunks: two lanes per pairing (k_miller_acc2) when the chunks hold one item each
 // and one lane per chunk would leave SIMDs idle (< 65,536 chunks = 1,024 waves), else one lane per chunk.
 void launch_miller_acc_auto(const PipelineBuffers& pb, bool units, hipStream_t st, uint32_t mk, int64_t lanes_opt) {
-  const bool two = lanes_opt == 2 || (lanes_opt == 0 && mk == 1 && pb.n_chunks < 65536);
-  if (two && mk == 1)
+  // two lanes per chunk: f never on one lane, no spills (r4zd/r4ze A/B, PMC r4f); auto: one-item chunks
+  const bool two = lanes_opt == 2 || (lanes_opt == 0 && mk == 1);
+  if (two)
     launch_miller_acc2(pb, units, st);
   else
     launch_miller_acc(pb, units, st);
@@ -770,7 +773,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     beg(kStages, sm);
     if (!coop) {
       // two lanes per message while one lane each would leave SIMDs idle (the same rule as the accumulation's)
-      const bool two = opt.miller_lanes == 2;  // measured: 2.9 ms vs 2.0 ms one-lane at 16k (r4l), lane exchange spills
+      const bool two = opt.lines_lanes == 2;  // measured: 2.9 ms vs 2.0 ms one-lane at 16k (r4l), lane exchange spills
       if (two)
         launch_miller_lines2(pb, sm);
       else
@@ -1858,6 +1861,9 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "msm_slice_mid") {
     if (value < 8 || value > MSM_SLICE) return BLSGPU_ERR_ARGS;
     ctx->opt.msm_slice_mid = value;
+  } else if (k == "lines_lanes") {
+    if (value < 1 || value > 2) return BLSGPU_ERR_ARGS;
+    ctx->opt.lines_lanes = value;
   } else if (k == "msm_tree") {
     ctx->opt.msm_tree = value != 0;
   } else if (k == "lane_tail_parts") {
@@ -1916,6 +1922,7 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "lane_tail_parts") *value = o.lane_tail_parts;
   else if (k == "msm_slice_mid") *value = o.msm_slice_mid;
   else if (k == "msm_tree") *value = o.msm_tree;
+  else if (k == "lines_lanes") *value = o.lines_lanes;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }
