@@ -154,9 +154,14 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * alternate between the device's two stream pairs, so two runs' message chains overlap and a third run's decode /
  * pubkey work fills the gaps; a deeper pipeline only queues), "merge_wait_us" (while runs are in
  * flight, a slot forming a run waits up to this long for more calls to merge, default 2000; an idle device starts
- * at once), "miller_lanes" (lanes per pairing of the one-item-chunk Miller accumulation: 0 = by run size, the default --
- * two lanes per pairing below 65,536 chunks, where one lane per pairing leaves SIMDs idle; 1; 2), "serial" (diagnostics: every branch of a run on one stream, so each kernel runs alone on the chip; 0/1,
- * default 0), "profile" (per-stage kernel times in
+ * at once), "idle_wait_us" (an idle device lingers up to this long while calls keep arriving, default 0), "miller_lanes" (lanes per Miller accumulation chunk: 0 = auto, the default -- two lanes
+ * for one-item chunks (each holding half of f), one lane for shared-squaring chunks; 1 = one lane; 2 = two lanes),
+ * "lines_lanes" (lanes per message of the Miller lines, 1 (default) or 2), "msm_slice_mid" (MSM slice length of runs
+ * of 1k-32k sets, 8..256, default 32), "msm_tree" (those runs sum each range's slices by a pairwise tree, 0/1,
+ * default 1), "f_run_max" (merged runs: longest lane-serial run of the F product tree, a power of two, default 16),
+ * "lane_tail_min" / "lane_tail_parts" (runs of >= lane_tail_min sets take lane forms of the Horner passes (bit 0)
+ * and of MillerLoop(-g1, S) (bit 1) instead of the cooperative workgroups; default 0 = never, parts 3), "serial"
+ * (diagnostics: every branch of a run on one stream, so each kernel runs alone on the chip; 0/1, default 0), "profile" (per-stage kernel times in
  * blsgpu_stats.stage_ms, 0/1), "group_policy" (0 = batch groups of >= group_sets sets, the default; 1 = the
  * reference pool's grouping: calls split into <= 128-set jobs (chunkifyMaximizeChunkSize(sets, 128),
  * multithread/index.ts:156), packed into >= 128-set worker requests (prepareWork, index.ts:386-401), each
