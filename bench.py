@@ -470,6 +470,7 @@ def main():
     ap.add_argument("--lane-tail-min", type=int, default=-1,
                     help="runs of >= this many sets use lane forms of the signature tails (-1 = runtime default, 0 never)")
     ap.add_argument("--lane-tail-parts", type=int, default=-1, help="bit 0 Horner, bit 1 MillerLoop(-g1, S)")
+    ap.add_argument("--merge-balance", type=int, default=-1, help="cut a backlog into equal runs (-1 = default)")
     ap.add_argument("--lines-lanes", type=int, default=0, help="lanes per message of the Miller lines (0 = default)")
     ap.add_argument("--msm-slice-mid", type=int, default=0, help="MSM slice length of 1k-32k-set runs (0 = default)")
     ap.add_argument("--msm-tree", type=int, default=-1, help="pairwise slice tree for those runs (-1 = default)")
@@ -520,6 +521,8 @@ def main():
         ctx.set_option("miller_lanes", args.miller_lanes)
     if args.f_run_max:
         ctx.set_option("f_run_max", args.f_run_max)
+    if args.merge_balance >= 0:
+        ctx.set_option("merge_balance", args.merge_balance)
     if args.lines_lanes:
         ctx.set_option("lines_lanes", args.lines_lanes)
     if args.msm_slice_mid:

@@ -154,7 +154,8 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * alternate between the device's two stream pairs, so two runs' message chains overlap and a third run's decode /
  * pubkey work fills the gaps; a deeper pipeline only queues), "merge_wait_us" (while runs are in
  * flight, a slot forming a run waits up to this long for more calls to merge, default 2000; an idle device starts
- * at once), "idle_wait_us" (an idle device lingers up to this long while calls keep arriving, default 0), "miller_lanes" (lanes per Miller accumulation chunk: 0 = auto, the default -- two lanes
+ * at once), "idle_wait_us" (an idle device lingers up to this long while calls keep arriving, default 0), "merge_balance"
+ * (a backlog above merge_sets is cut into equal runs, 0/1, default 0), "miller_lanes" (lanes per Miller accumulation chunk: 0 = auto, the default -- two lanes
  * for one-item chunks (each holding half of f), one lane for shared-squaring chunks; 1 = one lane; 2 = two lanes),
  * "lines_lanes" (lanes per message of the Miller lines, 1 (default) or 2), "msm_slice_mid" (MSM slice length of runs
  * of 1k-32k sets, 8..256, default 32), "msm_tree" (those runs sum each range's slices by a pairwise tree, 0/1,

@@ -204,6 +204,7 @@ struct Options {  // snapshot taken at the start of each call
   int64_t lane_tail_parts = 3;    // bit 0: Horner passes, bit 1: MillerLoop(-g1, S)
   int64_t msm_slice_mid = 32;     // MSM slice length of runs of 1k-32k sets
   int64_t lines_lanes = 1;        // lanes per message of the Miller lines (1, 2)
+  int64_t merge_balance = 0;      // a backlog above merge_sets is cut into equal runs
   int64_t msm_tree = 1;           // those runs sum each range's slices by a pairwise tree
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
@@ -211,7 +212,7 @@ struct Options {  // snapshot taken at the start of each call
            f_run_max == o.f_run_max && lane_tail_min == o.lane_tail_min &&
            lane_tail_parts == o.lane_tail_parts &&
            msm_slice_mid == o.msm_slice_mid && msm_tree == o.msm_tree &&
-           lines_lanes == o.lines_lanes;
+           lines_lanes == o.lines_lanes && merge_balance == o.merge_balance;
   }
 };
 
@@ -1449,7 +1450,17 @@ void worker_loop(Device* d, Slot* sl) {
       d->queue.pop_front();
       const Call* c0 = parts[0].call;
       uint32_t total = task_sets(parts[0]);
-      const int64_t cap = c0->opt.merge_sets;
+      int64_t cap = c0->opt.merge_sets;
+      // balanced runs: a backlog above the cap is cut into equal runs (19 queued 16k calls at a 131,072-set cap: 6 + 6
+      // + 7 calls instead of 8 + 8 + 3, so the last run of a burst is not a short one draining alone)
+      if (cap > 0 && c0->opt.merge_balance) {
+        int64_t backlog = total;
+        for (const Task& t : d->queue) backlog += task_sets(t);
+        if (backlog > cap) {
+          const int64_t runs = (backlog + cap - 1) / cap;
+          cap = (backlog + runs - 1) / runs;
+        }
+      }
       const auto t_start = std::chrono::steady_clock::now();
       const auto deadline = t_start + std::chrono::microseconds(c0->opt.merge_wait_us);
       // idle device: linger only while a burst keeps arriving -- each new call extends the wait by idle_wait_us / 4,
@@ -1861,6 +1872,8 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "msm_slice_mid") {
     if (value < 8 || value > MSM_SLICE) return BLSGPU_ERR_ARGS;
     ctx->opt.msm_slice_mid = value;
+  } else if (k == "merge_balance") {
+    ctx->opt.merge_balance = value != 0;
   } else if (k == "lines_lanes") {
     if (value < 1 || value > 2) return BLSGPU_ERR_ARGS;
     ctx->opt.lines_lanes = value;
@@ -1923,6 +1936,7 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "msm_slice_mid") *value = o.msm_slice_mid;
   else if (k == "msm_tree") *value = o.msm_tree;
   else if (k == "lines_lanes") *value = o.lines_lanes;
+  else if (k == "merge_balance") *value = o.merge_balance;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }
