@@ -12,6 +12,13 @@
 #include "k_common.hpp"
 #include "gt_wave.hpp"
 
+// Line pairs in the one-lane chunk loop (line_pair + fp12_mul_by_line2: 23 Fp2 products per two items instead of 26):
+// correct (test_line_pair_product, chunk-form GPU parity) but the pending line and the denser product raise the
+// kernel's scratch 480 -> 1,600 B/lane, and the driver's C2 measured 3.03M vs 3.06M without (r4zn): off.
+#ifndef BLS_LINE_PAIRS
+#define BLS_LINE_PAIRS 0
+#endif
+
 BLS_INL fp fp_add_n(const fp& a, const fp& b) { return fp_add_norm(a, b); }
 
 STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_miller_lines(PipelineBuffers b) {
@@ -116,6 +123,12 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc(PipelineBuffers b) {
   for (int s = 0; s < MILLER_STEPS; s++) {
     if (!add_next && s != 0) f = fp12_sqr(f);
     const uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
+#if BLS_LINE_PAIRS
+    // the chunk's lines two at a time: their product first (line_pair, 6 Fp2 products), then f times it (17) -- 23
+    // products per two items against 26 for two sparse products
+    bool pend = false;
+    fp2 q0, q1, q4;
+#endif
 #pragma unroll 1
     for (uint32_t k = k0; k < k1; k++) {
       const uint32_t i = b.chunk_items[k];
@@ -134,8 +147,24 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc(PipelineBuffers b) {
       L.l0 = ld_fp2(o, b.nm, m, 0);
       L.c1 = ld_fp2(o, b.nm, m, 2 * W_FP);
       L.c4 = ld_fp2(o, b.nm, m, 4 * W_FP);
+#if BLS_LINE_PAIRS
+      const fp2 l1 = fp2_mul_fp(L.c1, P.x), l4 = fp2_mul_fp(L.c4, P.y);
+      if (pend) {
+        f = fp12_mul_by_line2(f, line_pair(q0, q1, q4, L.l0, l1, l4));
+        pend = false;
+      } else {
+        q0 = L.l0;
+        q1 = l1;
+        q4 = l4;
+        pend = true;
+      }
+#else
       f = fp12_mul_by_014(f, L.l0, fp2_mul_fp(L.c1, P.x), fp2_mul_fp(L.c4, P.y));
+#endif
     }
+#if BLS_LINE_PAIRS
+    if (pend) f = fp12_mul_by_014(f, q0, q1, q4);
+#endif
     if (!add_next) {
       add_next = (BLS_Z_ABS >> bit) & 1ull;
       bit--;

@@ -386,6 +386,9 @@ BLS_BIG fp6 fp6_inv(const fp6& a) {
   return fp6_make(fp2_mul(t0, di), fp2_mul(t1, di), fp2_mul(t2, di));
 }
 
+// X - A - B component-wise as lazy combinations (terms: products, normalized, values <= 2p)
+#define F2_LC3(X, A, B) \
+  fp2_make(fp_lc(T<1>((X).c0), T<-1>((A).c0), T<-1>((B).c0)), fp_lc(T<1>((X).c1), T<-1>((A).c1), T<-1>((B).c1)))
 // --------------------------------------------------------------------------------------------- Fp12
 BLS_HD fp12 fp12_make(const fp6& a, const fp6& b) {
   fp12 r;
@@ -525,6 +528,79 @@ BLS_FN fp12 fp12_mul_by_014(const fp12& f, const fp2& l0, const fp2& l1, const f
   return fp12_make(c0, c1);
 }
 #endif
+
+// Two lines multiplied together first (the Miller accumulation's chunks of two pairings): (a0 + a1 v + a4 v w)
+// (b0 + b1 v + b4 v w) = (a0 b0 + xi a4 b4) + (a0 b1 + a1 b0) v + a1 b1 v^2 + (a0 b4 + a4 b0) v w + (a1 b4 + a4 b1) v^2 w
+// (w^2 = v, v^3 = xi): six Fp2 products (three squares of the pairs by Karatsuba), c1.c0 = 0.  Then f times that
+// element (fp12_mul_by_line2: 17 products) -- 23 in all against 26 for two sparse products.  Inputs normalized,
+// values <= 2p; outputs lazily reduced (fp_lc).
+BLS_FN fp12 line_pair(const fp2& a0, const fp2& a1, const fp2& a4, const fp2& b0, const fp2& b1, const fp2& b4) {
+  const fp2 P00 = fp2_mul(a0, b0), P11 = fp2_mul(a1, b1), P44 = fp2_mul(a4, b4);
+  fp12 m;
+  m.c0.c0 = fp2_make(fp_lc(T<1>(P00.c0), T<1>(P44.c0), T<-1>(P44.c1)), fp_lc(T<1>(P00.c1), T<1>(P44.c0), T<1>(P44.c1)));
+  m.c0.c2 = P11;
+  m.c1.c0 = fp2_zero();
+  {
+    const fp2 X = fp2_mul(fp2_add_nr(a0, a1), fp2_add_nr(b0, b1));
+    m.c0.c1 = F2_LC3(X, P00, P11);
+  }
+  {
+    const fp2 X = fp2_mul(fp2_add_nr(a0, a4), fp2_add_nr(b0, b4));
+    m.c1.c1 = F2_LC3(X, P00, P44);
+  }
+  {
+    const fp2 X = fp2_mul(fp2_add_nr(a1, a4), fp2_add_nr(b1, b4));
+    m.c1.c2 = F2_LC3(X, P11, P44);
+  }
+  return m;
+}
+
+// f * m with m.c1.c0 = 0 (a line_pair product): Karatsuba over Fp6, t1 = f1 m1 with m1 = (0, b1, b2) in five
+// products: c0 = xi (X - t1 - t2), c1 = (a0 + a1) b1 - t1 + xi t2, c2 = (a0 + a2) b2 - t2 + t1, X = (a1 + a2)(b1 + b2)
+BLS_FN fp6 fp6_mul_by_12(const fp6& a, const fp2& b1, const fp2& b2) {
+  const fp2 t1 = fp2_mul(a.c1, b1), t2 = fp2_mul(a.c2, b2);
+  fp6 r;
+  {
+    const fp2 X = fp2_mul(fp2_add_nr(a.c1, a.c2), fp2_add_nr(b1, b2));  // X - t1 - t2 = a1 b2 + a2 b1
+    r.c0.c0 = fp_lc(T<1>(X.c0), T<-1>(t1.c0), T<-1>(t2.c0), T<-1>(X.c1), T<1>(t1.c1), T<1>(t2.c1));
+    r.c0.c1 = fp_lc(T<1>(X.c0), T<-1>(t1.c0), T<-1>(t2.c0), T<1>(X.c1), T<-1>(t1.c1), T<-1>(t2.c1));
+  }
+  {
+    const fp2 Y = fp2_mul(fp2_add_nr(a.c0, a.c1), b1);
+    r.c1.c0 = fp_lc(T<1>(Y.c0), T<-1>(t1.c0), T<1>(t2.c0), T<-1>(t2.c1));
+    r.c1.c1 = fp_lc(T<1>(Y.c1), T<-1>(t1.c1), T<1>(t2.c0), T<1>(t2.c1));
+  }
+  {
+    const fp2 Z = fp2_mul(fp2_add_nr(a.c0, a.c2), b2);
+    r.c2.c0 = fp_lc(T<1>(Z.c0), T<-1>(t2.c0), T<1>(t1.c0));
+    r.c2.c1 = fp_lc(T<1>(Z.c1), T<-1>(t2.c1), T<1>(t1.c1));
+  }
+  return r;
+}
+BLS_FN fp12 fp12_mul_by_line2(const fp12& f, const fp12& m) {
+  const fp6 t0 = fp6_mul(f.c0, m.c0);
+  const fp6 t1 = fp6_mul_by_12(f.c1, m.c1.c1, m.c1.c2);
+  fp6 sa, sb;  // f0 + f1, m0 + m1 (normalized, values <= 4p: fp6_mul's operand contract)
+  sa.c0 = fp2_make(fp_add_norm(f.c0.c0.c0, f.c1.c0.c0), fp_add_norm(f.c0.c0.c1, f.c1.c0.c1));
+  sa.c1 = fp2_make(fp_add_norm(f.c0.c1.c0, f.c1.c1.c0), fp_add_norm(f.c0.c1.c1, f.c1.c1.c1));
+  sa.c2 = fp2_make(fp_add_norm(f.c0.c2.c0, f.c1.c2.c0), fp_add_norm(f.c0.c2.c1, f.c1.c2.c1));
+  sb.c0 = m.c0.c0;
+  sb.c1 = fp2_make(fp_add_norm(m.c0.c1.c0, m.c1.c1.c0), fp_add_norm(m.c0.c1.c1, m.c1.c1.c1));
+  sb.c2 = fp2_make(fp_add_norm(m.c0.c2.c0, m.c1.c2.c0), fp_add_norm(m.c0.c2.c1, m.c1.c2.c1));
+  const fp6 X = fp6_mul(sa, sb);
+  fp12 r;  // c0 = t0 + v t1 = (t0.c0 + xi t1.c2, t0.c1 + t1.c0, t0.c2 + t1.c1), c1 = X - t0 - t1
+  r.c0.c0 = fp2_make(fp_lc(T<1>(t0.c0.c0), T<1>(t1.c2.c0), T<-1>(t1.c2.c1)),
+                     fp_lc(T<1>(t0.c0.c1), T<1>(t1.c2.c0), T<1>(t1.c2.c1)));
+  r.c0.c1 = fp2_make(fp_lc(T<1>(t0.c1.c0), T<1>(t1.c0.c0)), fp_lc(T<1>(t0.c1.c1), T<1>(t1.c0.c1)));
+  r.c0.c2 = fp2_make(fp_lc(T<1>(t0.c2.c0), T<1>(t1.c1.c0)), fp_lc(T<1>(t0.c2.c1), T<1>(t1.c1.c1)));
+  r.c1.c0 = fp2_make(fp_lc(T<1>(X.c0.c0), T<-1>(t0.c0.c0), T<-1>(t1.c0.c0)),
+                     fp_lc(T<1>(X.c0.c1), T<-1>(t0.c0.c1), T<-1>(t1.c0.c1)));
+  r.c1.c1 = fp2_make(fp_lc(T<1>(X.c1.c0), T<-1>(t0.c1.c0), T<-1>(t1.c1.c0)),
+                     fp_lc(T<1>(X.c1.c1), T<-1>(t0.c1.c1), T<-1>(t1.c1.c1)));
+  r.c1.c2 = fp2_make(fp_lc(T<1>(X.c2.c0), T<-1>(t0.c2.c0), T<-1>(t1.c2.c0)),
+                     fp_lc(T<1>(X.c2.c1), T<-1>(t0.c2.c1), T<-1>(t1.c2.c1)));
+  return r;
+}
 
 // Squaring in the cyclotomic subgroup (Granger-Scott, eprint 2009/565 section 3.2): f^(p^6+1) = 1 lets
 // f^2 be computed from three Fp4 squarings -- 9 Fp2 squarings (18 Fp products) instead of 36.

@@ -478,3 +478,19 @@ extern "C" void emu_fp2_sqr_limbs(const uint32_t* in28, uint32_t* out28) {
     out28[14 + i] = r.c1.l[i];
   }
 }
+
+// f * l_a * l_b two ways: two sparse products (fp12_mul_by_014) and the line-pair form (line_pair, then
+// fp12_mul_by_line2); 1 when they are equal mod p.  in: f (576 B), then the six Fp2 line coefficients (6 x 96 B).
+extern "C" int emu_line_pair_check(const uint8_t* f576, const uint8_t* lines576) {
+  const fp12 f = load12(f576);
+  const fp2 a0 = load2(lines576), a1 = load2(lines576 + 96), a4 = load2(lines576 + 192);
+  const fp2 b0 = load2(lines576 + 288), b1 = load2(lines576 + 384), b4 = load2(lines576 + 480);
+  const fp12 x = fp12_mul_by_014(fp12_mul_by_014(f, a0, a1, a4), b0, b1, b4);
+  const fp12 y = fp12_mul_by_line2(f, line_pair(a0, a1, a4, b0, b1, b4));
+  uint8_t bx[576], by[576];
+  store12(x, bx);
+  store12(y, by);
+  for (int i = 0; i < 576; i++)
+    if (bx[i] != by[i]) return 0;
+  return 1;
+}

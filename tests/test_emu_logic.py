@@ -482,3 +482,18 @@ def test_fp2_sqr_operand_contract():
         assert c0 < 1.05 * P and c1 < 1.05 * P, (trial, c0 / P, c1 / P)
         assert c0 % P == (a0 * a0 - a1 * a1) * Rinv % P, trial
         assert c1 % P == 2 * a0 * a1 * Rinv % P, trial
+
+
+def test_line_pair_product():
+    """The Miller accumulation's chunks of two: f * (l_a * l_b) by line_pair + fp12_mul_by_line2 equals two sparse
+    products f * l_a * l_b (tower.hpp), on random Fp12 values and random line coefficients (host build)."""
+    import random
+
+    L = lib()
+    L.emu_line_pair_check.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    P = bls.P
+    rnd = random.Random(21)
+    for _ in range(200):
+        f = b"".join(rnd.randrange(P).to_bytes(48, "big") for _ in range(12))
+        lines = b"".join(rnd.randrange(P).to_bytes(48, "big") for _ in range(12))
+        assert L.emu_line_pair_check(f, lines) == 1
