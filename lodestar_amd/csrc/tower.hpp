@@ -90,6 +90,63 @@ BLS_INL fp2 fp2_mul_lazy_body(const fp& a0, const fp& a1, const fp& b0, const fp
   return r;
 }
 
+// 16p with limbs 0-12 borrowed up into [2^29, 2^30): 16p - b has no negative limb for b with limbs < 2^29 and a top
+// limb below 0x1a010e (values < 8p, normalized or one fp_add_nr level)
+BLS_CONST fp FP_16P_K = {{0x3ffaaab0, 0x3efffffc, 0x3ffffb9c, 0x3ffeb150, 0x3241eabc, 0x30f6b0f3, 0x36730d27, 0x338512bc,
+                          0x3774b84c, 0x3bacd761, 0x3a7b6431, 0x369a4b18, 0x3ea397fb, 0x001a010e}};
+// Fp2 product as two schoolbook column sums straight into the two Montgomery accumulators, no Karatsuba
+// recombination: c0 = Redc(a0 b0 + a1 (16p - b1)) (= a0 b0 - a1 b1 mod p), c1 = Redc(a0 b1 + a1 b0).  784 + 392
+// v_mad_u64_u32 against the lazy body's 980, but no 64-bit column subtractions (with their carry hazards), no signed
+// accumulator and no operand sums: fewer instruction slots and registers per product.  Inputs as fp2_mul_lazy_body
+// (limbs < 2^29, values < 8p); column bound 14 (2^58 + 2^59) + 14 * 2^56 + 2^36 < 2^64; outputs normalized, < 1.1 p.
+BLS_INL fp2 fp2_mul_sb_body(const fp& a0, const fp& a1, const fp& b0, const fp& b1) {
+  uint32_t nb[BLS_NL], m0[BLS_NL], m1[BLS_NL];
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) nb[i] = FP_16P_K.l[i] - b1.l[i];
+  uint64_t acc0 = 0, acc1 = 0;
+  fp2 r;
+#pragma unroll
+  for (int k = 0; k < 2 * BLS_NL - 1; k++) {
+    const int lo = k < BLS_NL ? 0 : k - BLS_NL + 1, hi = k < BLS_NL ? k : BLS_NL - 1;
+#pragma unroll
+    for (int i = lo; i <= hi; i++) {
+      acc0 += (uint64_t)a0.l[i] * b0.l[k - i];
+      acc1 += (uint64_t)a0.l[i] * b1.l[k - i];
+      acc0 += (uint64_t)a1.l[i] * nb[k - i];
+      acc1 += (uint64_t)a1.l[i] * b0.l[k - i];
+    }
+    const int mhi = k < BLS_NL ? k - 1 : BLS_NL - 1;
+#pragma unroll
+    for (int i = lo; i <= mhi; i++) {
+      acc0 += (uint64_t)m0[i] * FP_P.l[k - i];
+      acc1 += (uint64_t)m1[i] * FP_P.l[k - i];
+    }
+    if (k < BLS_NL) {
+      const uint32_t q0 = ((uint32_t)acc0 * BLS_N0INV) & BLS_MASK, q1 = ((uint32_t)acc1 * BLS_N0INV) & BLS_MASK;
+      m0[k] = q0;
+      m1[k] = q1;
+      acc0 += (uint64_t)q0 * FP_P.l[0];
+      acc1 += (uint64_t)q1 * FP_P.l[0];
+    } else {
+      r.c0.l[k - BLS_NL] = (uint32_t)acc0 & BLS_MASK;
+      r.c1.l[k - BLS_NL] = (uint32_t)acc1 & BLS_MASK;
+    }
+    acc0 >>= BLS_LB;
+    acc1 >>= BLS_LB;
+  }
+  r.c0.l[BLS_NL - 1] = (uint32_t)acc0;
+  r.c1.l[BLS_NL - 1] = (uint32_t)acc1;
+  return r;
+}
+#ifndef BLS_FP2_SB
+#define BLS_FP2_SB 1
+#endif
+#if BLS_FP2_SB
+#define fp2_mul_body_sel fp2_mul_sb_body
+#else
+#define fp2_mul_body_sel fp2_mul_lazy_body
+#endif
+
 // Fp2 squaring (complex method): c0 = (a0 + a1)(a0 - a1), c1 = 2 a0 a1 -- two independent products.  Input:
 // normalized limbs, values <= 4p (stored values, or fp2_add_norm of two); a0 - a1 goes to the product as
 // a0 + 8p - a1 (fp_sub_k8, no reduction), so an input above 2p never underflows.  Outputs < 1.05 p.
@@ -125,7 +182,7 @@ __device__ __noinline__ fp2_ret fp2_mul_r(BLS_PARAMS14(a), BLS_PARAMS14(c)) {
     y0.l[i] = bls_fp2_arg[i * BLS_FP2_LDS_LANES + t];
     y1.l[i] = bls_fp2_arg[(BLS_NL + i) * BLS_FP2_LDS_LANES + t];
   }
-  const fp2 r = fp2_mul_lazy_body(x0, x1, y0, y1);
+  const fp2 r = fp2_mul_body_sel(x0, x1, y0, y1);
   fp2_ret o;
 #pragma unroll
   for (int i = 0; i < BLS_NL; i++) {
@@ -210,7 +267,7 @@ BLS_FN fp2 fp2_sqr(const fp2& a) {
 BLS_FN fp2 fp2_mul_fp(const fp2& a, const fp& s) { return fp2_make(fp_mul(a.c0, s), fp_mul(a.c1, s)); }
 BLS_FN fp2 fp2_mul(const fp2& a, const fp2& b) {
   BLS_COUNT5(bls_count_half);  // 3 half-products + 2 reductions, each half a Montgomery multiplication
-  return fp2_mul_lazy_body(a.c0, a.c1, b.c0, b.c1);
+  return fp2_mul_body_sel(a.c0, a.c1, b.c0, b.c1);
 }
 BLS_FN fp2 fp2_sqr(const fp2& a) {
   BLS_COUNT(bls_count_mul);

@@ -494,3 +494,18 @@ extern "C" int emu_line_pair_check(const uint8_t* f576, const uint8_t* lines576)
     if (bx[i] != by[i]) return 0;
   return 1;
 }
+// the schoolbook-offset Fp2 product body on raw limbs (same layout as emu_fp2_mul_lazy_limbs)
+extern "C" void emu_fp2_mul_sb_limbs(const uint32_t* in56, uint32_t* out28) {
+  fp a0, a1, b0, b1;
+  for (int i = 0; i < BLS_NL; i++) {
+    a0.l[i] = in56[i];
+    a1.l[i] = in56[14 + i];
+    b0.l[i] = in56[28 + i];
+    b1.l[i] = in56[42 + i];
+  }
+  const fp2 r = fp2_mul_sb_body(a0, a1, b0, b1);
+  for (int i = 0; i < BLS_NL; i++) {
+    out28[i] = r.c0.l[i];
+    out28[14 + i] = r.c1.l[i];
+  }
+}

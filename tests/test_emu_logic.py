@@ -497,3 +497,26 @@ def test_line_pair_product():
         f = b"".join(rnd.randrange(P).to_bytes(48, "big") for _ in range(12))
         lines = b"".join(rnd.randrange(P).to_bytes(48, "big") for _ in range(12))
         assert L.emu_line_pair_check(f, lines) == 1
+
+
+def test_fp2_mul_schoolbook_offset_bounds():
+    """tower.hpp fp2_mul_sb_body (c0 = Redc(a0 b0 + a1 (16p - b1)), c1 = Redc(a0 b1 + a1 b0)) on raw limbs at the
+    edges of the same contract (limbs < 2^29, values < 8p): the Fp2 product / R mod p, normalized, below 1.1 p."""
+    L = lib()
+    L.emu_fp2_mul_sb_limbs.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    r2 = random.Random(4343)
+    RINV = pow(2**392, -1, P)
+    edge = [0, 1, P - 1, P, 2 * P, 8 * P - 1, 8 * P - 2**300, 2**383]
+    out = (ctypes.c_uint32 * 28)()
+    for it in range(3000):
+        vals = [r2.choice(edge) if r2.random() < 0.3 else r2.randrange(8 * P) for _ in range(4)]
+        limbs = [x for v in vals for x in _limbs_of(v, r2)]
+        L.emu_fp2_mul_sb_limbs((ctypes.c_uint32 * 56)(*limbs), out)
+        o = list(out)
+        assert all(x < 2**28 for x in o), (vals, o)
+        c0 = sum(x << (28 * i) for i, x in enumerate(o[:14]))
+        c1 = sum(x << (28 * i) for i, x in enumerate(o[14:]))
+        a0, a1, b0, b1 = vals
+        assert c0 < 1.1 * P and c1 < 1.1 * P, (vals,)
+        assert c0 % P == (a0 * b0 - a1 * b1) * RINV % P, (it, vals)
+        assert c1 % P == (a0 * b1 + a1 * b0) * RINV % P, (it, vals)

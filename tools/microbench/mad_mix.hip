@@ -1,5 +1,5 @@
 // What a non-MAD instruction costs beside v_mad_u64_u32 at one wave per SIMD (gfx950): 32 MADs per iteration into
-// four independent 64-bit accumulators, interleaved with F independent filler instructions per MAD of one kind --
+// four independent 64-bit accumulators (carry-out SGPR pairs rotated), interleaved with F independent filler instructions per MAD of one kind --
 // v_add_u32, a 64-bit add as v_add_co_u32 + v_addc_co_u32 (counted as two), or v_lshl_add_u64 -- at 1 and 2 waves
 // per SIMD.  Prints SIMD cycles per iteration and per MAD as JSON.  Decides whether trading MADs for additions
 // (Karatsuba column sums) pays on this issue-bound path.
@@ -38,7 +38,13 @@ __global__ __launch_bounds__(64) void k_mix(uint64_t* out, uint32_t s) {
   for (int it = 0; it < ITERS; it++) {
 #pragma unroll
     for (int j = 0; j < MADS; j++) {
-      asm volatile("v_mad_u64_u32 %0, s[40:41], %1, %2, %0" : "+v"(acc[j & 3]) : "v"(a), "v"(b) : "s40", "s41");
+      // carry-out SGPR pairs rotated over four (one shared pair serializes the MADs: the compiler rotates too)
+      switch (j & 3) {
+        case 0: asm volatile("v_mad_u64_u32 %0, s[40:41], %1, %2, %0" : "+v"(acc[0]) : "v"(a), "v"(b) : "s40", "s41"); break;
+        case 1: asm volatile("v_mad_u64_u32 %0, s[42:43], %1, %2, %0" : "+v"(acc[1]) : "v"(a), "v"(b) : "s42", "s43"); break;
+        case 2: asm volatile("v_mad_u64_u32 %0, s[44:45], %1, %2, %0" : "+v"(acc[2]) : "v"(a), "v"(b) : "s44", "s45"); break;
+        default: asm volatile("v_mad_u64_u32 %0, s[46:47], %1, %2, %0" : "+v"(acc[3]) : "v"(a), "v"(b) : "s46", "s47"); break;
+      }
 #pragma unroll
       for (int f = 0; f < F; f++) {
         const int q = (j * F + f) & 7;
