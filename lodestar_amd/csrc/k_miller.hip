@@ -18,6 +18,13 @@
 #ifndef BLS_LINE_PAIRS
 #define BLS_LINE_PAIRS 0
 #endif
+// Line pairs in the two-lane accumulation: the pair's line product split three and three over the lanes, then each
+// lane one half of f times it (6 + 5 Fp2 products): 14 products per lane per two items instead of 16.  Correct (the
+// chunk-form parity tests pass with it) but the pending line and M spill (1,280 B/lane): forced two-lane chunks of
+// two measured 2.92M vs 3.47M for the default one-lane form (100 steps): off.
+#ifndef BLS_ACC2_PAIRS
+#define BLS_ACC2_PAIRS 0
+#endif
 
 BLS_INL fp fp_add_n(const fp& a, const fp& b) { return fp_add_norm(a, b); }
 
@@ -228,6 +235,20 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc2(PipelineBuffers b) {
       mine = fp6_xlane(r);  // lane 0 computed c1', lane 1 c0': swap back
     }
     const uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
+    // mine <- mine-half of f * (T0 + T1 w) given T0 = mine x M0-part, T1 = other x M1-part: lane 0 c0' = T0 + v T1,
+    // lane 1 c1' = T0 + T1
+    auto fold = [&](const fp6& T0, const fp6& T1) {
+      const fp6 T1v = h ? T1 : fp6_mul_v(T1);
+      fp6 r;
+      r.c0 = fp2_make(fp_lc(T<1>(T0.c0.c0), T<1>(T1v.c0.c0)), fp_lc(T<1>(T0.c0.c1), T<1>(T1v.c0.c1)));
+      r.c1 = fp2_make(fp_lc(T<1>(T0.c1.c0), T<1>(T1v.c1.c0)), fp_lc(T<1>(T0.c1.c1), T<1>(T1v.c1.c1)));
+      r.c2 = fp2_make(fp_lc(T<1>(T0.c2.c0), T<1>(T1v.c2.c0)), fp_lc(T<1>(T0.c2.c1), T<1>(T1v.c2.c1)));
+      mine = r;
+    };
+#if BLS_ACC2_PAIRS
+    bool pend = false;
+    fp2 q0, q1, q4;
+#endif
 #pragma unroll 1
     for (uint32_t k = k0; k < k1; k++) {
       const uint32_t i = b.chunk_items[k];
@@ -245,17 +266,42 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc2(PipelineBuffers b) {
       const fp2 l0 = ld_fp2(o, b.nm, m, 0);
       const fp2 l1 = fp2_mul_fp(ld_fp2(o, b.nm, m, 2 * W_FP), P.x);
       const fp2 l4 = fp2_mul_fp(ld_fp2(o, b.nm, m, 4 * W_FP), P.y);
+#if BLS_ACC2_PAIRS
+      if (!pend) {
+        q0 = l0;
+        q1 = l1;
+        q4 = l4;
+        pend = true;
+        continue;
+      }
+      pend = false;
+      // the two lines' product (tower.hpp line_pair) split over the pair: lane 0 P00, P11, X01, lane 1 P44, X04, X14
+      const fp2 R1 = fp2_mul(h ? q4 : q0, h ? l4 : l0);
+      const fp2 R2 = fp2_mul(h ? fp2_add_nr(q0, q4) : q1, h ? fp2_add_nr(l0, l4) : l1);
+      const fp2 R3 = fp2_mul(h ? fp2_add_nr(q1, q4) : fp2_add_nr(q0, q1), h ? fp2_add_nr(l1, l4) : fp2_add_nr(l0, l1));
+      const fp2 O1 = fp2_xlane(R1), O2 = fp2_xlane(R2), O3 = fp2_xlane(R3);
+      const fp2 P00 = h ? O1 : R1, P44 = h ? R1 : O1, P11 = h ? O2 : R2, X04 = h ? R2 : O2, X01 = h ? O3 : R3,
+                X14 = h ? R3 : O3;
+      fp6 M0;
+      M0.c0 = fp2_make(fp_lc(T<1>(P00.c0), T<1>(P44.c0), T<-1>(P44.c1)), fp_lc(T<1>(P00.c1), T<1>(P44.c0), T<1>(P44.c1)));
+      M0.c1 = F2_LC3(X01, P00, P11);
+      M0.c2 = P11;
+      const fp2 m11 = F2_LC3(X04, P00, P44), m12 = F2_LC3(X14, P11, P44);
+      // f * M (M1 = (0, m11, m12)): lane 0 c0' = f0 M0 + v f1 M1, lane 1 c1' = f1 M0 + f0 M1
+      const fp6 other = fp6_xlane(mine);
+      fold(fp6_mul(mine, M0), fp6_mul_by_12(other, m11, m12));
+#else
       // lane 0: c0' = c0 (l0 + l1 v) + v (c1 (l4 v)); lane 1: c1' = c1 (l0 + l1 v) + c0 (l4 v)
       const fp6 other = fp6_xlane(mine);
-      const fp6 A = fp6_mul_by_01(mine, l0, l1);  // own half times (l0 + l1 v)
-      const fp6 Z = fp6_mul_by_1(other, l4);
-      const fp6 Zv = h ? Z : fp6_mul_v(Z);
-      fp6 r;
-      r.c0 = fp2_make(fp_lc(T<1>(A.c0.c0), T<1>(Zv.c0.c0)), fp_lc(T<1>(A.c0.c1), T<1>(Zv.c0.c1)));
-      r.c1 = fp2_make(fp_lc(T<1>(A.c1.c0), T<1>(Zv.c1.c0)), fp_lc(T<1>(A.c1.c1), T<1>(Zv.c1.c1)));
-      r.c2 = fp2_make(fp_lc(T<1>(A.c2.c0), T<1>(Zv.c2.c0)), fp_lc(T<1>(A.c2.c1), T<1>(Zv.c2.c1)));
-      mine = r;
+      fold(fp6_mul_by_01(mine, l0, l1), fp6_mul_by_1(other, l4));
+#endif
     }
+#if BLS_ACC2_PAIRS
+    if (pend) {  // an odd item: its sparse product alone
+      const fp6 other = fp6_xlane(mine);
+      fold(fp6_mul_by_01(mine, q0, q1), fp6_mul_by_1(other, q4));
+    }
+#endif
     if (!add_next) {
       add_next = (BLS_Z_ABS >> bit) & 1ull;
       bit--;

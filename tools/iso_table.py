@@ -23,7 +23,7 @@ def main(path, n, k=2):
         "hash_to_g2": (["k_hash_prep", "k_hash_map", "k_hash_clear", "k_h_affine", "k_batch_inv"],
                        ps["hash_to_g2"]["total"] * n),
         "pk_finish": (["k_pk_finish", "k_pk_affine"], ps["pk_finish"]["total"] * n),
-        "sig_msm": (["k_msm_bucket", "k_msm_window", "k_msm_horner"],
+        "sig_msm": (["k_msm_bucket", "k_msm_slice_pairs", "k_msm_window", "k_msm_horner"],
                     ps["sig_msm"]["total"] * n + ops["per_group_fixed"]["sig_msm"] * groups),
         "miller_lines": (["k_miller_lines", "k_miller_lines2"], ops["miller_lines_per_message"] * n),
         "miller_acc": (["k_miller_acc", "k_miller_acc2"], ops["miller_acc_per_chunk"][str(k)] * n / k),
