@@ -8,6 +8,9 @@
 //                   (P = r_i pk_i) or, with same-message merging, a unit: the included sets of one batch
 //                   group that sign the same root (P = sum r_i pk_i; the pairing is bilinear, so
 //                   prod_i e(r_i pk_i, H(m)) = e(sum_i r_i pk_i, H(m))).
+//   k_miller_acc2:  the same accumulation on TWO lanes per chunk, each holding half of f (no spills): the default
+//                   for one-item chunks (runs below 131,072 pairings); chunks of >= 2 stay on one lane (faster).
+//   k_miller_lines2 (two lanes per message) and k_miller_coop (one 192-lane workgroup per pairing, small runs).
 // Line traffic is 68 x 84 words = 22.8 KB per message (HBM-cheap next to ~5,200 Montgomery products).
 #include "k_common.hpp"
 #include "gt_wave.hpp"
