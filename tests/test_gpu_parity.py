@@ -429,3 +429,46 @@ def test_miller_chunk_forms_vs_oracle(ctx, k, lanes):
         ctx.set_option("miller_k", 0)
         ctx.set_option("miller_lanes", 0)
     assert (got == 1).sum() >= n - max(8, n // 100) and st.batch_retries >= 1
+
+
+@pytest.mark.parametrize("slice_len,tree", [(8, 1), (32, 1), (32, 0), (128, 1)])
+def test_msm_slice_forms_vs_oracle(ctx, slice_len, tree):
+    """The MSM of 1k-32k-set runs at other slice lengths, with and without the pairwise slice tree, on a 2,048-set
+    call with ~1% corrupted sets: job for job equal to the oracle."""
+    n = 2048
+    rng = np.random.default_rng(7 * slice_len + tree)
+    sks, pks, msgs, sigs, sig_len = corrupted_single_sets(n, b"MS", rng)
+    base = dict(sigs=sigs, sig_len=sig_len, msgs=b"".join(msgs), sig_stride=192)
+    ctx.set_option("msm_slice_mid", slice_len)
+    ctx.set_option("msm_tree", tree)
+    try:
+        got, st = compare(ctx, job_first_set=np.arange(n + 1), pk_bytes=pks, job_flags=np.ones(n), **base)
+    finally:
+        ctx.set_option("msm_slice_mid", 32)
+        ctx.set_option("msm_tree", 1)
+    assert (got == 1).sum() >= n - max(8, n // 100) and st.batch_retries >= 1
+
+
+def test_balanced_merging_keeps_answers():
+    """merge_balance cuts a backlog of queued calls into equal runs; every call keeps its own answer."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from lodestar_amd.native import Context
+
+    n = 1024
+    rng = np.random.default_rng(33)
+    sks, pks, msgs, sigs, sig_len = corrupted_single_sets(n, b"bal", rng)
+    c = Context([0])
+    try:
+        c.set_option("merge_balance", 1)
+        c.set_option("merge_sets", 3 * n)
+        c.upload_pubkeys(0, pks)
+        call = dict(job_first_set=np.arange(n + 1), sigs=sigs, sig_len=sig_len, msgs=b"".join(msgs),
+                    set_pk_first=np.arange(n + 1), pk_index=np.arange(n), job_flags=np.ones(n), sig_stride=192)
+        want, _ = cpu.verify_jobs(table=cpu.Table(pks), threads=THREADS, **call)
+        with ThreadPoolExecutor(10) as pool:
+            outs = [f.result() for f in [pool.submit(c.verify_raw, **call) for _ in range(10)]]
+        for got, st in outs:
+            assert np.array_equal(got, want)
+    finally:
+        c.close()
