@@ -472,3 +472,18 @@ def test_balanced_merging_keeps_answers():
             assert np.array_equal(got, want)
     finally:
         c.close()
+
+
+def test_two_lane_lines_vs_oracle(ctx):
+    """The two-lanes-per-message Miller lines (k_miller_lines2, lines_lanes 2) on a 2,048-set call with ~1% corrupted
+    sets: job for job equal to the oracle."""
+    n = 2048
+    rng = np.random.default_rng(99)
+    sks, pks, msgs, sigs, sig_len = corrupted_single_sets(n, b"L2", rng)
+    base = dict(sigs=sigs, sig_len=sig_len, msgs=b"".join(msgs), sig_stride=192)
+    ctx.set_option("lines_lanes", 2)
+    try:
+        got, st = compare(ctx, job_first_set=np.arange(n + 1), pk_bytes=pks, job_flags=np.ones(n), **base)
+    finally:
+        ctx.set_option("lines_lanes", 1)
+    assert (got == 1).sum() >= n - max(8, n // 100)
