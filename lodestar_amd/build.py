@@ -3,6 +3,7 @@
     python -m lodestar_amd.build            # incremental
     python -m lodestar_amd.build --force
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -77,10 +78,14 @@ def build(force=False, verbose=True):
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include")]
     defines = os.environ.get("BLSGPU_DEFINES", "").split()  # e.g. BLSGPU_WPE=2
     common += ["-D" + d for d in defines]
+    cflags = os.environ.get("BLSGPU_CFLAGS", "").split()  # tuning variants: extra compiler flags
+    common += cflags
     tu_defs = tu_defines()
     os.makedirs(OBJ_DIR, exist_ok=True)
     # objects are keyed by the library name and the defines, so variant builds never reuse each other's objects
     key = os.path.splitext(os.path.basename(LIB))[0] + ("." + "_".join(defines).replace("=", "-") if defines else "")
+    if cflags:
+        key += ".cf" + hashlib.md5(" ".join(cflags).encode()).hexdigest()[:8]
     # one translation unit per pipeline stage, compiled in parallel (the stage kernels are large)
     procs = []
     t0 = time.time()
