@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define BLSGPU_ABI_VERSION 5
+#define BLSGPU_ABI_VERSION 6
 
 enum blsgpu_code {
   BLSGPU_OK = 0,
@@ -110,6 +110,9 @@ typedef struct blsgpu_stats {
                                calls into one run reports it (and stage_ms) on the first call, 0 on the others */
   uint32_t run_calls;       /* calls served by the pipeline run of this call's (first) shard: 1 = ran alone, k > 1 =
                                merged with k - 1 other queued calls (set on every call of the run) */
+  uint32_t fallback_jobs;   /* clean jobs of failed groups re-checked on their own (the run's, like run_sets) */
+  uint32_t fallback_miller; /* Miller loops the fallback recomputed: 0 when it reused the batch pass's per-set values
+                               (per-set pairings, no same-message units) */
 } blsgpu_stats;
 
 /* Create a context on the given HIP devices (NULL / n <= 0: every visible device).  Each device runs
@@ -212,7 +215,9 @@ int blsgpu_shard_jobs(const uint32_t* job_first_set, const uint32_t* set_pk_firs
  * randomness.  Pure host code. */
 int blsgpu_batch_scalars(const blsgpu_batch* b, uint64_t* words);
 
-/* Test hook: fault injection, process-wide.  After `skip` more events, the next `count` events fail:
+/* Test hook: fault injection, process-wide, available only when the process was started with the environment
+ * variable BLSGPU_FAULT_INJECTION=1 (read once; otherwise every call returns BLSGPU_ERR_ARGS and nothing is armed).
+ * After `skip` more events, the next `count` events fail:
  *   BLSGPU_INJECT_ENTROPY: an entropy draw (seed-0 calls, blsgpu_batch_scalars) -> BLSGPU_ERR_ENTROPY;
  *   BLSGPU_INJECT_DEVICE: a pipeline run, once its batch pass completed, as if a HIP call had failed -> every job
  *     of every call in that run -BLSGPU_DEVICE_ERROR (never 0); the dispatcher keeps serving later calls.

@@ -32,10 +32,12 @@ inline uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
   a += b, d ^= a, d = rotl(d, 8);  \
   c += d, b ^= c, b = rotl(b, 7)
 
-// One ChaCha20 block (RFC 8439 §2.3): key, 32-bit block counter, 96-bit nonce (fixed 0: every key serves one call)
-inline void chacha20_block(const Key& key, uint32_t counter, uint32_t out[16]) {
+// One ChaCha20 block (RFC 8439 §2.3): key, 32-bit block counter, 96-bit nonce.  Every key serves one call; the nonce
+// separates the keystreams a call draws: nonce 0 = the batch scalar words, kNonceHashKey = the message index's hash key.
+constexpr uint32_t kNonceHashKey = 0x68736b31u;  // "1ksh"
+inline void chacha20_block(const Key& key, uint32_t counter, uint32_t out[16], uint32_t nonce0 = 0) {
   uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key.k[0], key.k[1], key.k[2], key.k[3],
-                    key.k[4],    key.k[5],    key.k[6],    key.k[7],    counter,  0u,       0u,       0u};
+                    key.k[4],    key.k[5],    key.k[6],    key.k[7],    counter,  nonce0,   0u,       0u};
   uint32_t x[16];
   memcpy(x, s, sizeof x);
   for (int r = 0; r < 10; r++) {
@@ -98,6 +100,15 @@ inline bool os_key(Key& key) {
 inline Key seed_key(uint64_t seed) {
   return Key{{(uint32_t)seed, (uint32_t)(seed >> 32), 0x65646f6cu, 0x72617473u, 0x646d612du, 0x61637320u,
               0x2072616cu, 0x7379656bu}};
+}
+
+// The message index's hash key (runtime.cpp MsgIndex): 64 bits of the call key's own keystream under a separate nonce,
+// so no key word of the scalars' keystream ever drives the host hash table (a timing leak of the table would reveal
+// nothing about the scalars).
+inline uint64_t hash_key(const Key& key) {
+  uint32_t blk[16];
+  chacha20_block(key, 0, blk, kNonceHashKey);
+  return (uint64_t)blk[0] | ((uint64_t)blk[1] << 32);
 }
 
 // Scalar words [first, first + n) of the call keyed by `key` -> out[0 .. n)

@@ -147,14 +147,14 @@ __global__ __launch_bounds__(WAVE) void k_hash_clear_coop(PipelineBuffers b) {
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
-void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s, bool coop) {
+void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s, bool coop, bool exclusive) {
   if (!b.n_umsg) return;
   hipLaunchKernelGGL(k_hash_prep, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
   launch_batch_inv(b.h_norm, b.nm, 0, b.inv_buf, b.n_umsg, s);
   hipLaunchKernelGGL(k_hash_map, grid_for(2 * b.n_umsg), dim3(WAVE), 0, s, b, b.inv_buf);
   if (coop)
     hipLaunchKernelGGL(k_hash_clear_coop, dim3((b.n_umsg + HC_GROUPS - 1) / HC_GROUPS), dim3(WAVE),
-                       BLSGPU_EXCLUSIVE_SMALL ? exclusive_cu_lds<k_hash_clear_coop>() : 0, s, b);
+                       BLSGPU_EXCLUSIVE_SMALL && exclusive ? exclusive_cu_lds<k_hash_clear_coop>() : 0, s, b);
   else
     hipLaunchKernelGGL(k_hash_clear, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
 }

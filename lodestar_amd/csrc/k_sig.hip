@@ -84,13 +84,14 @@ void launch_spec_mask(const PipelineBuffers& b, uint32_t n, uint8_t* spec, hipSt
   if (n) hipLaunchKernelGGL(k_spec_mask, grid_for(n), dim3(WAVE), 0, s, b, n, spec);
 }
 
-void launch_sig_decode(const PipelineBuffers& b, uint32_t n, hipStream_t s, bool coop, hipEvent_t decoded) {
+void launch_sig_decode(const PipelineBuffers& b, uint32_t n, hipStream_t s, bool coop, hipEvent_t decoded,
+                       bool exclusive) {
   if (!n) return;
   hipLaunchKernelGGL(k_sig_decode, grid_for(n), dim3(WAVE), 0, s, b, n, !coop);
   if (decoded) (void)hipEventRecord(decoded, s);
   if (coop)
     hipLaunchKernelGGL(k_sig_subgroup_coop, dim3((n + SG_GROUPS - 1) / SG_GROUPS), dim3(WAVE),
-                       BLSGPU_EXCLUSIVE_SMALL ? exclusive_cu_lds<k_sig_subgroup_coop>() : 0, s, b, n);
+                       BLSGPU_EXCLUSIVE_SMALL && exclusive ? exclusive_cu_lds<k_sig_subgroup_coop>() : 0, s, b, n);
 }
 void launch_sig_scale(const PipelineBuffers& b, uint32_t n, hipStream_t s, const uint32_t* list) {
   if (n) hipLaunchKernelGGL(k_sig_scale, grid_for(n), dim3(WAVE), 0, s, b, n, list);

@@ -83,14 +83,16 @@ struct PipelineBuffers {
   uint8_t* include;   // [n]: set belongs to a clean job (enters the batch equation)
 };
 
-// coop: small runs -- the [|z|] chains (subgroup check, cofactor clearing) as cooperative 16-lane doublings
-// (g2_coop.hpp), for latency
+// coop: small and mid-size runs -- the [|z|] chains (subgroup check, cofactor clearing) as cooperative 16-lane
+// doublings (g2_coop.hpp), for latency; exclusive: each cooperative workgroup takes a CU to itself (small runs only:
+// beyond ~one workgroup per CU the padding serializes the launch)
 // (decoded: recorded after the decode, before the small-run subgroup checks)
 void launch_sig_decode(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s, bool coop = false,
-                       hipEvent_t decoded = nullptr);
+                       hipEvent_t decoded = nullptr, bool exclusive = true);
 // spec[i] = the signature of set i decoded (the speculative MSM's include mask)
 void launch_spec_mask(const PipelineBuffers& b, uint32_t n_sets, uint8_t* spec, hipStream_t s);
-void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s, bool coop = false);  // over the unique messages
+void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s, bool coop = false,
+                       bool exclusive = true);  // over the unique messages
 void launch_pk_aggregate(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 void launch_pk_finish(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s);
 // batched affine conversions (Montgomery's simultaneous inversion, k_inv.hip): r_i pk_i -> pk_aff, H(m) -> h_aff

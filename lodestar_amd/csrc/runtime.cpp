@@ -108,13 +108,14 @@ inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 // (Device::st) and are shared by its slots, so a device needs kStreams hardware queues whatever its slot count.
 struct Slot {
   hipEvent_t join_in = nullptr, join_msg = nullptr, join_pk = nullptr, join_mask = nullptr, join_gsm = nullptr,
-             join_dec = nullptr, join_msm = nullptr, done = nullptr;  // no timing
+             join_dec = nullptr, join_msm = nullptr, join_rsig = nullptr, done = nullptr;  // no timing
   hipEvent_t ev[2 * (kStages + 2)] = {};  // profile: (start, end) per stage; pairs kStages, kStages + 1 = the
                                           // Miller lines, the groups' MillerLoop(-g1, S) (parts of stages 5, 7)
   // d_in / h_in: every per-call input packed into one arena (one H2D transfer); d_res / h_res: job errors +
   // group verdicts (one D2H transfer).
   DevBuf<uint8_t> d_in, d_res, d_bytes, d_ok;
   DevBuf<uint32_t> d_work, d_lines, d_S, d_F, d_G, d_list, d_msmB, d_msmW, d_fb;
+  DevBuf<uint32_t> d_fkeep;  // the batch pass's per-set Miller values, kept for the fallback (run_shard keep_f)
   HostBuf<uint8_t> h_in, h_res, h_ok;
   HostBuf<uint32_t> h_list;
   bool retire = false;     // set under the device queue lock: the dispatcher exits instead of taking work
@@ -125,12 +126,12 @@ struct Slot {
   // whenever it grows a buffer (its dispatcher waits for each run), so only this ordering matters
   void set_stream(hipStream_t st) {
     for (auto* b : {&d_in, &d_res, &d_bytes, &d_ok}) b->st = st;
-    for (auto* b : {&d_work, &d_lines, &d_S, &d_F, &d_G, &d_list, &d_msmB, &d_msmW, &d_fb}) b->st = st;
+    for (auto* b : {&d_work, &d_lines, &d_S, &d_F, &d_G, &d_list, &d_msmB, &d_msmW, &d_fb, &d_fkeep}) b->st = st;
   }
   void release_all() {
     d_in.release(); d_res.release(); d_bytes.release(); d_ok.release();
     d_work.release(); d_lines.release(); d_S.release(); d_F.release(); d_list.release();
-    d_msmB.release(); d_msmW.release(); d_fb.release(); d_G.release();
+    d_msmB.release(); d_msmW.release(); d_fb.release(); d_G.release(); d_fkeep.release();
     h_in.release(); h_res.release(); h_ok.release(); h_list.release();
   }
 };
@@ -206,13 +207,18 @@ struct Options {  // snapshot taken at the start of each call
   int64_t lines_lanes = 1;        // lanes per message of the Miller lines (1, 2)
   int64_t merge_balance = 0;      // a backlog above merge_sets is cut into equal runs
   int64_t msm_tree = 1;           // those runs sum each range's slices by a pairwise tree
+  int64_t coop_max = 2048;        // runs of <= this many pairings take the cooperative Miller loops (k_miller_coop)
+  int64_t coop_g2_max = 4096;     // runs of <= this many sets take the cooperative [|z|] chains (clearing, subgroup)
+  int64_t coop_excl_max = 512;    // cooperative workgroups take a CU each only in runs of <= this many items
+  int64_t rsig_spec = 1;          // small idle runs form every r_i sig_i beside the batch pass (for the fallback)
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
            group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&
            f_run_max == o.f_run_max && lane_tail_min == o.lane_tail_min &&
            lane_tail_parts == o.lane_tail_parts &&
            msm_slice_mid == o.msm_slice_mid && msm_tree == o.msm_tree &&
-           lines_lanes == o.lines_lanes && merge_balance == o.merge_balance;
+           lines_lanes == o.lines_lanes && merge_balance == o.merge_balance && coop_max == o.coop_max &&
+           coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec;
   }
 };
 
@@ -291,7 +297,7 @@ struct Call {
   Owned* owned = nullptr;
   int8_t* job_result = nullptr;
   blsgpu_stats* stats = nullptr;
-  uint64_t seed = 0;       // message-index hash key (comparison runs: the batch seed)
+  uint64_t seed = 0;       // message-index hash key (batch_rand::hash_key of the call key)
   batch_rand::Key key{};   // batch scalars: ChaCha20 keystream under this key (batch_rand.hpp)
   uint32_t max_index = 0;  // largest pubkey-table index of the call (table mode)
   Options opt;
@@ -517,11 +523,15 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   }
   const uint32_t n_units = merged ? (uint32_t)unit_msg.size() : 0;
   // Miller chunks of the batch pass: each group's items (sets, or units) in chunks of miller_k
-  // Small runs (<= kCoopMaxItems pairings, miller_k auto or 1): one cooperative workgroup per pairing (k_miller_coop,
-  // lines on the fly) -- 1/6 of the lane-per-chunk loop's latency, at a fraction of its lane efficiency.
-  constexpr uint32_t kCoopMaxItems = 512;
+  // Small and mid-size runs (<= opt.coop_max pairings, miller_k auto or 1): one cooperative workgroup per pairing
+  // (k_miller_coop, lines on the fly) -- 1/6 of the lane-per-chunk loop's latency, at a fraction of its lane
+  // efficiency.  The [|z|] chains of the cofactor clearing and the subgroup check go cooperative below opt.coop_g2_max
+  // sets.  Up to opt.coop_excl_max items every cooperative workgroup takes a CU to itself (k_common.hpp
+  // exclusive_cu_lds): with more workgroups than CUs the padding would serialize them.
   const uint32_t n_items = merged ? n_units : n;
-  const bool coop = n_items <= kCoopMaxItems && opt.miller_k <= 1;
+  const bool coop = n_items <= (uint32_t)opt.coop_max && opt.miller_k <= 1;
+  const bool coop_g2 = n <= (uint32_t)opt.coop_g2_max;
+  const bool excl = BLSGPU_EXCLUSIVE_SMALL && n_items <= (uint32_t)opt.coop_excl_max;
   const uint32_t mk = coop ? 1u : opt.miller_k > 0 ? (uint32_t)opt.miller_k : miller_k_auto(n_items);
   std::vector<uint32_t> chunk_first{0}, chunk_items, g_chunks(2 * (size_t)ng0);
   chunk_items.reserve(n);
@@ -533,6 +543,16 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     g_chunks[2 * g + 1] = cr.second;
   }
   const uint32_t n_chunks = (uint32_t)chunk_first.size() - 1;
+  // Per-set pairings (no same-message units, one item per chunk): chunk c is set c (the groups cover every set of a
+  // non-empty job, in order), so the batch pass's Miller values f_c = MillerLoop(r_c pk_c, H(m_c)) are exactly what a
+  // failed group's per-job checks need.  They are copied aside before the F tree multiplies chunks in place, and the
+  // fallback takes F_j = prod of its sets' kept values instead of re-running the Miller loops.
+  const bool keep_f = !merged && mk == 1 && n_chunks == n;
+  const bool spec = BLSGPU_STREAM_PAIRS && coop && sl.alone && !opt.serial;  // speculative MSM (kernel pipeline below)
+  // A small run on an idle device also forms every r_i sig_i (k_sig_scale) on the idle pubkey stream once its pubkeys
+  // and the decode are done: the chip has room, and a failed group's per-job checks then start from the sums instead
+  // of a 1.7 ms scaling launch on the fallback's critical path (the batch pass itself never reads them).
+  const bool rsig_spec = spec && opt.rsig_spec;
   // MSM slices of the groups' set ranges (S_g = sum r_i sig_i).  Runs up to 32k sets (an isolated block's or
   // gossip call's latency) take half slices: twice the bucket workgroups at half the chain, 16k isolated sig_msm
   // 3.55 -> 2.80 ms; merged runs keep full slices (fewer bucket sums to combine: 100-step C2 3.13M vs 3.01M).
@@ -551,8 +571,12 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     add_slices(slices, range_slices, job_sets(group_jobs[g].first).first, job_sets(group_jobs[g].second - 1).second,
                slice_len);
   const uint32_t n_slices = (uint32_t)(slices.size() / 2);
-  if (n > kMsmSmallSliceMaxSets && n <= kMsmHalfSliceMaxSets && opt.msm_tree)
+  if (n > kMsmSmallSliceMaxSets && n <= kMsmHalfSliceMaxSets && opt.msm_tree) {
     for (uint32_t g = 0; g < ng0; g++) msm_tree = std::max(msm_tree, range_slices[g + 1] - range_slices[g]);
+    // the tree's launches are sized n_ranges x (most slices of a range): only when the ranges are about equal (one
+    // large job beside many single-set groups would launch ~n_ranges x max_pairs idle lanes per level)
+    if ((uint64_t)ng0 * msm_tree > 2ull * n_slices) msm_tree = 0;
+  }
   // F_g = prod of the group's Miller chunks as a product tree (launch_group_tree): with more than 16384 chunks (merged
   // runs), runs of f_k consecutive chunks first (lane-serial: a 128-lane cooperative product costs ~6x the lane
   // time) down to <= 8192 heads, then pair levels of stride f_k, 2 f_k, ... (one cooperative workgroup per pair);
@@ -676,6 +700,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   const size_t per_set = W_G2A + W_G1J + W_G1A + W_FP12 + 8 * W_G1J + 2 * W_FP + (merged ? W_G1A : 0);
   sl.d_work.ensure((size_t)stride * per_set + (size_t)nm * (W_G2A + W_G2J + W_FP + 14 * W_FP + 2 * W_G2J));
   sl.d_lines.ensure((size_t)nm * kMillerLineWords);
+  if (keep_f) sl.d_fkeep.ensure((size_t)stride * W_FP12);
+  if (rsig_spec) sl.d_fb.ensure((size_t)stride * 9 * W_G2J);
   uint8_t* const din = sl.d_in.p;
   uint8_t* const d_ok0 = sl.d_res.p + o_ok;
 
@@ -743,7 +769,6 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // short next to the message branch; see sp below for small runs) and consecutive runs use the other pair; without,
   // each branch has its own stream shared by every run.
   const bool prof = opt.profile;
-  const bool spec = BLSGPU_STREAM_PAIRS && coop && sl.alone && !opt.serial;  // speculative MSM (below)
   // Large (merged) runs meet a chip full of one-wave-per-SIMD stage kernels: the signature branch's cooperative tails
   // (Horner passes, MillerLoop(-g1, S)) waited for free SIMD groups there, so they run on single lanes
   const bool lane_tail = opt.lane_tail_min > 0 && n >= (uint32_t)opt.lane_tail_min;
@@ -768,7 +793,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     HIPCHK(hipStreamWaitEvent(sp, sl.join_in, 0));
     // messages
     beg(1, sm);
-    launch_hash_to_g2(pb, sm, coop);
+    launch_hash_to_g2(pb, sm, coop_g2, excl);
     launch_h_affine(pb, sm);
     end(1, sm);
     beg(kStages, sm);
@@ -802,10 +827,19 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     PipelineBuffers pbm = pb;
     if (spec) pbm.include = db + ob_spec;
     beg(0, s);
-    launch_sig_decode(pb, n, s, coop, spec ? sl.join_dec : nullptr);
+    launch_sig_decode(pb, n, s, coop_g2, spec ? sl.join_dec : nullptr, excl);
     end(0, s);
     const uint32_t* d_slices = reinterpret_cast<uint32_t*>(din + o_slices);
     const uint32_t* d_rslices = reinterpret_cast<uint32_t*>(din + o_rslices);
+    if (rsig_spec) {  // after the pubkey branch on sp (its own work comes first) and the decode (+ subgroup checks)
+      HIPCHK(hipEventRecord(sl.join_rsig, s));
+      HIPCHK(hipStreamWaitEvent(sp, sl.join_rsig, 0));
+      PipelineBuffers pq = pb;
+      pq.rsig = sl.d_fb.p;
+      pq.scal_tab = sl.d_fb.p + (size_t)stride * W_G2J;
+      launch_sig_scale(pq, n, sp);
+      HIPCHK(hipEventRecord(sl.join_rsig, sp));
+    }
     if (spec) {
       HIPCHK(hipStreamWaitEvent(smsm, sl.join_dec, 0));
       launch_spec_mask(pb, n, pbm.include, smsm);
@@ -822,10 +856,12 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     beg(5, sm);
     if (merged) launch_unit_aggregate(pb, sm);
     if (coop)
-      launch_miller_coop(pb, merged, sm, BLSGPU_EXCLUSIVE_SMALL);
+      launch_miller_coop(pb, merged, sm, excl);
     else
       launch_miller_acc_auto(pb, merged, sm, mk, opt.miller_lanes);
     end(5, sm);
+    if (keep_f)
+      HIPCHK(hipMemcpyAsync(sl.d_fkeep.p, pb.f_chunk, (size_t)stride * W_FP12 * 4, hipMemcpyDeviceToDevice, sm));
     const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
     beg(6, sm);
     const uint32_t* d_ftree = reinterpret_cast<uint32_t*>(din + o_ftree);
@@ -840,14 +876,15 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     end(4, s);
     // MillerLoop(-g1, S_g) of every group now, while the message branch still runs
     beg(kStages + 1, s);
-    launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, s, BLSGPU_EXCLUSIVE_SMALL && coop,
+    launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, s, excl && coop,
                             lane_tail && (opt.lane_tail_parts & 2));
     end(kStages + 1, s);
     HIPCHK(hipEventRecord(sl.join_gsm, s));
     HIPCHK(hipStreamWaitEvent(stl, sl.join_gsm, 0));
     HIPCHK(hipStreamWaitEvent(stl, sl.join_msg, 0));
+    if (rsig_spec) HIPCHK(hipStreamWaitEvent(stl, sl.join_rsig, 0));  // the run completes with its r_i sig_i
     beg(7, stl);
-    launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, stl, nullptr, 0, sl.d_G.p, BLSGPU_EXCLUSIVE_SMALL && coop);
+    launch_group_check(sl.d_S.p, sl.d_F.p, ng0, d_ok0, stl, nullptr, 0, sl.d_G.p, excl && coop);
     end(7, stl);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(sl.h_res.p, sl.d_res.p, o_ok + ng0, hipMemcpyDeviceToHost, stl));
@@ -958,12 +995,23 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       rr[2 * q + 1] = js.second;
       add_slices(rsl, rrs, js.first, js.second);
       for (uint32_t i = js.first; i < js.second; i++) rset.push_back(i);
+      if (keep_f) {  // F_j from the kept per-set values: chunk = set
+        rf[2 * q] = js.first;
+        rf[2 * q + 1] = js.second;
+        continue;
+      }
       const auto cr = add_chunks(rfirst, ritems, js.first, js.second, mk);
       rf[2 * q] = cr.first;
       rf[2 * q + 1] = cr.second;
     }
-    const bool small_jobs = rset.size() < (size_t)32 * nr;  // per-set scalings instead of per-job MSMs
-    const uint32_t nsub = nr >= 2 * kFbSub ? (nr + kFbSub - 1) / kFbSub : 0;
+    // per-set scalings instead of per-job MSMs (or the speculative batch-pass scalings, when the run made them)
+    const bool small_jobs = rsig_spec || rset.size() < (size_t)32 * nr;
+    // A small run (cooperative forms: the chip is far from full) checks every retried job directly in ONE launch --
+    // up to kFbDirectMax checks run side by side (4 cooperative workgroups per CU) -- instead of sub-groups, a host
+    // round trip and then the jobs of the failing sub-groups: one check round instead of two.
+    constexpr uint32_t kFbDirectMax = 1024;
+    const bool direct = coop && nr <= kFbDirectMax;
+    const uint32_t nsub = !direct && nr >= 2 * kFbSub ? (nr + kFbSub - 1) / kFbSub : 0;
     std::vector<uint32_t> subr(2 * (size_t)nsub);
     for (uint32_t t = 0; t < nsub; t++) {
       subr[2 * t] = t * kFbSub;
@@ -998,16 +1046,23 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     pr.n_chunks = nc;
     pr.chunk_first = sl.d_list.p + 4 * (size_t)nr;
     pr.chunk_items = sl.d_list.p + 4 * (size_t)nr + rfirst.size();
-    if (coop)  // no stored lines in a cooperative run: the per-job chunks hold one set each (mk = 1)
-      launch_miller_coop(pr, false, stl);
-    else
-      launch_miller_acc_auto(pr, false, stl, mk, opt.miller_lanes);
+    if (keep_f) {
+      pr.f_chunk = sl.d_fkeep.p;  // the batch pass's values: no Miller loop is recomputed
+    } else {
+      st.fallback_miller += (uint32_t)ritems.size();
+      if (coop)  // no stored lines in a cooperative run: the per-job chunks hold one set each (mk = 1)
+        launch_miller_coop(pr, false, stl);
+      else
+        launch_miller_acc_auto(pr, false, stl, mk, opt.miller_lanes);
+    }
+    st.fallback_jobs += nr;
     if (small_jobs) {
-      // r_i sig_i for the retried sets (G2 window tables and results in the fallback's own buffers)
-      sl.d_fb.ensure((size_t)stride * 9 * W_G2J);
+      // r_i sig_i for the retried sets (G2 window tables and results in the fallback's own buffers), unless the batch
+      // pass already formed them (rsig_spec)
+      if (!rsig_spec) sl.d_fb.ensure((size_t)stride * 9 * W_G2J);
       pr.rsig = sl.d_fb.p;
       pr.scal_tab = sl.d_fb.p + (size_t)stride * W_G2J;
-      launch_sig_scale(pr, (uint32_t)rset.size(), stl, sl.d_list.p + o_rset);
+      if (!rsig_spec) launch_sig_scale(pr, (uint32_t)rset.size(), stl, sl.d_list.p + o_rset);
       launch_group_reduce_lane(pr, sl.d_list.p, sl.d_list.p + 2 * (size_t)nr, nr, dS, dF, stl);
     } else {
       sl.d_msmB.ensure((size_t)MSM_BUCKET_WORDS * std::max<uint32_t>(nrs, 1));
@@ -1102,6 +1157,8 @@ void finish_call(Call* c) {
     local.unique_messages += c->sst[k].unique_messages;
     local.pairing_units += c->sst[k].pairing_units;
     local.miller_chunks += c->sst[k].miller_chunks;
+    local.fallback_jobs += c->sst[k].fallback_jobs;
+    local.fallback_miller += c->sst[k].fallback_miller;
     if (c->rc[k] != BLSGPU_OK && c->rc[k] != BLSGPU_DEVICE_ERROR) status = c->rc[k];
   }
   local.run_sets = c->sst.empty() ? 0 : c->sst[0].run_sets;
@@ -1532,7 +1589,8 @@ void free_slot(Device* d, Slot* s) {
   if (last) (void)hipStreamSynchronize(last);
   for (auto& e : s->ev)
     if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk, s->join_mask, s->join_gsm, s->join_dec, s->join_msm, s->done})
+  for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk, s->join_mask, s->join_gsm, s->join_dec, s->join_msm,
+                       s->join_rsig, s->done})
     if (e) (void)hipEventDestroy(e);
   delete s;
 }
@@ -1543,7 +1601,7 @@ void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet sh
   try {
     s->set_stream(d->st[kSig]);
     for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk, &s->join_mask, &s->join_gsm, &s->join_dec, &s->join_msm,
-                          &s->done})
+                          &s->join_rsig, &s->done})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
   } catch (HipError&) {
@@ -1656,10 +1714,10 @@ void launch_call(blsgpu_ctx* ctx, Call* c) {
 bool resolve_key(uint64_t seed, batch_rand::Key& key, uint64_t& hash_key) {
   if (seed == 0) {
     if (!batch_rand::os_key(key)) return false;
-    hash_key = (uint64_t)key.k[6] | ((uint64_t)key.k[7] << 32);
+    hash_key = batch_rand::hash_key(key);  // its own keystream block, not key material
   } else {
     key = batch_rand::seed_key(seed);
-    hash_key = seed;
+    hash_key = batch_rand::hash_key(key);
   }
   return true;
 }
@@ -1879,6 +1937,17 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
     ctx->opt.lines_lanes = value;
   } else if (k == "msm_tree") {
     ctx->opt.msm_tree = value != 0;
+  } else if (k == "coop_max") {
+    if (value < 0 || value > (1 << 24)) return BLSGPU_ERR_ARGS;
+    ctx->opt.coop_max = value;
+  } else if (k == "coop_g2_max") {
+    if (value < 0 || value > (1 << 24)) return BLSGPU_ERR_ARGS;
+    ctx->opt.coop_g2_max = value;
+  } else if (k == "coop_excl_max") {
+    if (value < 0 || value > (1 << 24)) return BLSGPU_ERR_ARGS;
+    ctx->opt.coop_excl_max = value;
+  } else if (k == "rsig_spec") {
+    ctx->opt.rsig_spec = value != 0;
   } else if (k == "lane_tail_parts") {
     if (value < 0 || value > 3) return BLSGPU_ERR_ARGS;
     ctx->opt.lane_tail_parts = value;
@@ -1937,6 +2006,10 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "msm_tree") *value = o.msm_tree;
   else if (k == "lines_lanes") *value = o.lines_lanes;
   else if (k == "merge_balance") *value = o.merge_balance;
+  else if (k == "coop_max") *value = o.coop_max;
+  else if (k == "coop_g2_max") *value = o.coop_g2_max;
+  else if (k == "coop_excl_max") *value = o.coop_excl_max;
+  else if (k == "rsig_spec") *value = o.rsig_spec;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }
@@ -2056,7 +2129,12 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* b, int8_t* job_result, bl
 
 int blsgpu_batch_scalars(const blsgpu_batch* b, uint64_t* words) {
   if (!b || !b->job_first_set || (b->n_sets && !words)) return BLSGPU_ERR_ARGS;
-  if (b->n_jobs && b->job_first_set[b->n_jobs] != b->n_sets) return BLSGPU_ERR_ARGS;
+  // the job structure validate_batch requires (first entry 0, non-decreasing, last == n_sets): shard_scalars writes
+  // out[first set of a job] for single-set jobs, which must stay inside words[0 .. n_sets)
+  if (b->n_jobs == 0 ? b->n_sets != 0 : (b->job_first_set[0] != 0 || b->job_first_set[b->n_jobs] != b->n_sets))
+    return BLSGPU_ERR_ARGS;
+  for (uint32_t j = 0; j < b->n_jobs; j++)
+    if (b->job_first_set[j + 1] < b->job_first_set[j]) return BLSGPU_ERR_ARGS;
   batch_rand::Key key;
   uint64_t hash_key = 0;
   if (!resolve_key(b->seed, key, hash_key)) return BLSGPU_ERR_ENTROPY;
@@ -2065,7 +2143,12 @@ int blsgpu_batch_scalars(const blsgpu_batch* b, uint64_t* words) {
 }
 
 int blsgpu_debug_inject(int what, int64_t skip, int64_t count) {
-  if (skip < 0 || count < 0) return BLSGPU_ERR_ARGS;
+  // a process-wide failure switch: armed only in processes started with BLSGPU_FAULT_INJECTION=1 (tests), read once
+  static const bool enabled = [] {
+    const char* v = getenv("BLSGPU_FAULT_INJECTION");
+    return v && v[0] == '1' && v[1] == 0;
+  }();
+  if (!enabled || skip < 0 || count < 0) return BLSGPU_ERR_ARGS;
   if (what == BLSGPU_INJECT_ENTROPY) {
     batch_rand::inject_count() = 0;
     batch_rand::inject_skip() = skip;

@@ -80,6 +80,8 @@ class Stats(ctypes.Structure):
         ("miller_chunks", ctypes.c_uint32),
         ("run_sets", ctypes.c_uint32),
         ("run_calls", ctypes.c_uint32),
+        ("fallback_jobs", ctypes.c_uint32),
+        ("fallback_miller", ctypes.c_uint32),
     ]
 
 
@@ -176,7 +178,9 @@ def batch_scalars(job_first_set, job_flags=None, seed=0):
     """The batch scalar words a call would use (C-ABI blsgpu_batch_scalars, pure host code): uint64 array, one word
     per set (0 = r = 1).  Raises RuntimeError(ERR_ENTROPY) when seed is 0 and the OS gives no randomness."""
     jfs = np.ascontiguousarray(job_first_set, dtype=np.uint32)
-    n = int(jfs[-1]) if len(jfs) else 0
+    if len(jfs) == 0:
+        raise ValueError("job_first_set needs n_jobs + 1 >= 1 entries")
+    n = int(jfs[-1])
     b = Batch()
     b.n_sets = n
     b.n_jobs = len(jfs) - 1

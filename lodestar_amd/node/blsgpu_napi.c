@@ -447,7 +447,11 @@ static napi_value ModuleInit(napi_env env, napi_value exports) {
       {"keyValidate", NULL, KeyValidate, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"debugInject", NULL, DebugInject, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
   };
-  napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
+  /* the fault-injection test hook is exported only to processes started with BLSGPU_FAULT_INJECTION=1 (the library
+   * refuses to arm it otherwise) */
+  const char* fi = getenv("BLSGPU_FAULT_INJECTION");
+  const int with_inject = fi && fi[0] == '1' && fi[1] == 0;
+  napi_define_properties(env, exports, sizeof props / sizeof props[0] - (with_inject ? 0 : 1), props);
   napi_value v;
   napi_create_int32(env, BLSGPU_ABI_VERSION, &v);
   napi_set_named_property(env, exports, "abiVersion", v);

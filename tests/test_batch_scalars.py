@@ -113,3 +113,70 @@ def test_no_constant_scalar_fallback_in_runtime():
     src += open(os.path.join(ROOT, "lodestar_amd", "csrc", "batch_rand.hpp")).read()
     assert "4c4f444553544152" not in src.lower()
     assert "splitmix" not in src.lower()
+
+
+def _raw_batch_scalars(jfs, n_sets, n_jobs=None):
+    """blsgpu_batch_scalars on a raw job list (no Python-side checks): (rc, words)."""
+    import ctypes
+
+    jfs = np.ascontiguousarray(jfs, dtype=np.uint32)
+    b = native.Batch()
+    b.n_sets = n_sets
+    b.n_jobs = len(jfs) - 1 if n_jobs is None else n_jobs
+    b.job_first_set = jfs.ctypes.data
+    b.seed = 3
+    guard = np.full(max(n_sets, 1) + 16, 0xABABABABABABABAB, np.uint64)  # canaries past n_sets
+    rc = native.load().blsgpu_batch_scalars(ctypes.byref(b), guard.ctypes.data)
+    return rc, guard
+
+
+@pytest.mark.parametrize("jfs,n_sets", [
+    ([0, 5, 6, 3], 3),      # non-monotone: a single-set job would write words[5]
+    ([1, 2, 3], 3),         # does not start at 0
+    ([0, 2, 4], 3),         # does not end at n_sets
+    ([0], 2),               # no jobs but sets
+])
+def test_batch_scalars_rejects_malformed_jobs(jfs, n_sets):
+    """blsgpu_batch_scalars applies validate_batch's job_first_set rules before writing any word."""
+    rc, guard = _raw_batch_scalars(jfs, n_sets)
+    assert rc == native.ERR_ARGS
+    assert (guard == 0xABABABABABABABAB).all()  # nothing written
+
+
+def test_batch_scalars_python_rejects_empty_job_list():
+    with pytest.raises(ValueError):
+        native.batch_scalars(np.zeros(0, np.uint32))
+
+
+def test_batch_scalars_accepts_empty_jobs():
+    rc, guard = _raw_batch_scalars([0, 0, 2, 2, 3], 3)
+    assert rc == native.OK
+    assert (guard[3:] == 0xABABABABABABABAB).all()
+
+
+def test_hash_key_is_not_scalar_key_material():
+    """the message index's hash key is its own ChaCha20 block (nonce "1ksh"), not key words of the scalar
+    keystream's key (batch_rand.hpp hash_key, runtime.cpp resolve_key)."""
+    src = open(os.path.join(ROOT, "lodestar_amd", "csrc", "runtime.cpp")).read()
+    assert "key.k[6]" not in src and "key.k[7]" not in src
+    assert "batch_rand::hash_key(key)" in src
+
+
+def test_fault_injection_needs_the_environment_switch():
+    """blsgpu_debug_inject is armed only in a process started with BLSGPU_FAULT_INJECTION=1."""
+    import subprocess
+    import sys
+
+    code = ("from lodestar_amd import native\n"
+            "import sys\n"
+            "try:\n"
+            "    native.debug_inject(native.INJECT_ENTROPY, 0, 1)\n"
+            "except ValueError:\n"
+            "    sys.exit(7)\n"
+            "sys.exit(0)\n")
+    env = {k: v for k, v in os.environ.items() if k != "BLSGPU_FAULT_INJECTION"}
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env)
+    assert r.returncode == 7
+    env["BLSGPU_FAULT_INJECTION"] = "1"
+    r = subprocess.run([sys.executable, "-c", code + ""], cwd=ROOT, env=env)
+    assert r.returncode == 0

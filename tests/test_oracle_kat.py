@@ -68,8 +68,9 @@ def test_mainnet_block_signatures_decompress():
     packages/beacon-node/test/unit/sync/backfill/blocks.json, copied as tests/golden/mainnet_g2_points.json)
     and selection proofs (state-transition/test/unit/util/aggregator.test.ts:28,37)."""
     with open(os.path.join(GOLDEN, "mainnet_g2_points.json")) as fh:
-        pts = json.load(fh)["points"]
-    assert len(pts) >= 8
+        fx = json.load(fh)
+    pts = fx["points"]
+    assert len(pts) == len(set(pts)) >= 55 and fx["count_blocks_json"] == 53  # every G2 encoding blocks.json holds
     for h in pts:
         b = bytes.fromhex(h)
         pt = bls.signature_from_bytes(b)  # decompress + subgroup check, must not raise
