@@ -479,6 +479,8 @@ def main():
     ap.add_argument("--sets", type=int, default=0, help="diagnostics: sets per call of C1/C2 (default the config's)")
     ap.add_argument("--serial", action="store_true",
                     help="diagnostics: every branch of a run on one stream (each kernel alone on the chip)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="any other runtime option (blsgpu_set_option), e.g. --set coop_max=1024; repeatable")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
@@ -533,6 +535,9 @@ def main():
         ctx.set_option("lane_tail_parts", args.lane_tail_parts)
     if args.lane_tail_min >= 0:
         ctx.set_option("lane_tail_min", args.lane_tail_min)
+    for kv in args.set:
+        k, _, v = kv.partition("=")
+        ctx.set_option(k, int(v))
     work, n_sets, desc, pk_per_set = build_workload(ctx, args.config, rank, world, n_dev, sets=args.sets)
     expected = work.pop("expected", None)
     if expected is None:

@@ -20,6 +20,9 @@
  *   blsgpu_signing_roots            <- computeSigningRoot (state-transition/src/util/signingRoot.ts:7-13)
  *   blsgpu_shard_jobs               <- the job sharding rule the runtime applies over devices (also restated
  *                                      by lodestar_amd/shard.py for one-process-per-GPU launches)
+ *   blsgpu_route_call               <- which devices a call runs on (whole on the least-loaded device below
+ *                                      "route_split_sets" sets, else split); the pool's worker choice
+ *                                      (multithread/index.ts:386-401 prepareWork + the free-worker pick)
  *
  * Conventions: plain pointers and sizes, caller-owned buffers, every call copies its inputs before
  * returning (blsgpu_submit included), `int` status (0 = ok).  Per-job results use the blst error names
@@ -163,6 +166,11 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * "lines_lanes" (lanes per message of the Miller lines, 1 (default) or 2), "msm_slice_mid" (MSM slice length of runs
  * of 1k-32k sets, 8..256, default 32), "msm_tree" (those runs sum each range's slices by a pairwise tree, 0/1,
  * default 1), "f_run_max" (merged runs: longest lane-serial run of the F product tree, a power of two, default 16),
+ * "coop_max" / "coop_g2_max" (runs of <= this many pairings / sets take the cooperative Miller loops / [|z|] chains,
+ * default 2048 / 4096), "coop_excl_max" (cooperative workgroups take a CU each in runs of <= this many items, default
+ * 512), "rsig_spec" (small idle runs form every r_i sig_i beside the batch pass for a possible fallback, 0/1, default
+ * 1), "fb_lane_min" (fallback check launches of >= this many checks in large runs take one lane per check, default
+ * 256, 0 = never), "route_split_sets" (see blsgpu_route_call, default 16384),
  * "lane_tail_min" / "lane_tail_parts" (runs of >= lane_tail_min sets take lane forms of the Horner passes (bit 0)
  * and of MillerLoop(-g1, S) (bit 1) instead of the cooperative workgroups; default 0 = never, parts 3), "serial"
  * (diagnostics: every branch of a run on one stream, so each kernel runs alone on the chip; 0/1, default 0), "profile" (per-stage kernel times in
@@ -208,6 +216,14 @@ int blsgpu_signing_roots(blsgpu_ctx* ctx, int kind, uint32_t n, const uint8_t* o
  * cost-balanced parts (cost = sets + aggregated pubkeys / 256; set_pk_first nullable).  Pure host code. */
 int blsgpu_shard_jobs(const uint32_t* job_first_set, const uint32_t* set_pk_first, uint32_t n_jobs,
                       uint32_t n_parts, uint32_t* part_first_job);
+
+/* The runtime's call routing: a call of n_sets sets goes to k = min(n_devices, max(1, n_sets / split_sets)) devices
+ * (option "route_split_sets", default 16384: a gossip call runs whole on one device, an epoch-scale call splits), the
+ * k least loaded by device_load[] (cost of their queued and running shards), ties broken by distance from `start`;
+ * out_devices[0 .. k) in shard order (ascending), *n_out = k.  Pure host code (lodestar_amd/shard.py route_call
+ * restates it). */
+int blsgpu_route_call(uint32_t n_sets, uint32_t n_devices, const int64_t* device_load, int64_t split_sets,
+                      uint32_t start, uint32_t* out_devices, uint32_t* n_out);
 
 /* The batch scalar words blsgpu_verify would use for `b` (only n_sets, n_jobs, job_first_set, job_flags and seed
  * are read): words[i] for set i, 0 = r = 1 (a single-set non-batchable job: CoreVerify).  With seed 0 every call

@@ -158,6 +158,26 @@ __global__ __launch_bounds__(MILLER ? GTW_MILLER_LANES : GTW_LANES) void k_group
   if (t == 0) ok[blockIdx.x] = fp12_is_one(gtw_to_reg(sh.F)) ? 1 : 0;
 }
 
+// The same check on ONE lane per entry (pairing.hpp miller_loop + final_exponentiation): ~64x the cooperative form's
+// latency per check but a few percent of its chip time -- for the fallback of merged runs under load, where thousands
+// of checks at once left the cooperative workgroups contending for SIMDs at ~1% of the VALU peak (r05 trace: 3,424
+// checks in 36-46 ms) while one wave of lanes takes 64 checks on one SIMD.
+STAGE_KERNEL_W(BLSGPU_WPE_GRP) void k_group_check_lane(const uint32_t* S_in, const uint32_t* F_in, uint32_t ng,
+                                                      const uint32_t* sel, uint32_t n, uint8_t* ok) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  if (q >= n) return;
+  const uint32_t g = sel ? sel[q] : q;
+  fp12 F = ld_fp12(F_in, ng, g);
+  g2a Sa;
+  if (jac_to_aff(ld_g2j(S_in, ng, g), Sa)) {
+    g1a P;
+    P.x = G1_GEN_X;
+    P.y = G1_NEG_GEN_Y;
+    F = fp12_mul(F, miller_loop(P, Sa));
+  }
+  ok[q] = fp12_is_one(final_exponentiation(F)) ? 1 : 0;
+}
+
 // Fallback sub-groups: S_out[r] = sum S_in[e], F_out[r] = prod F_in[e] over the entries e of range r
 // (entries = per-job values, stride n_in; one wave per range, strided partials + LDS tree).
 __global__ __launch_bounds__(WAVE) void k_range_combine(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in,
@@ -255,10 +275,12 @@ void launch_group_tree(const PipelineBuffers& b, const uint32_t* f_ranges, uint3
   hipLaunchKernelGGL(k_f_gather, grid_for(ng * W_FP12), dim3(WAVE), 0, s, b, f_ranges, ng, F);
 }
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s,
-                        const uint32_t* sel, uint32_t n_sel, const uint32_t* G, bool exclusive) {
+                        const uint32_t* sel, uint32_t n_sel, const uint32_t* G, bool exclusive, bool lane) {
   const uint32_t n = sel ? n_sel : ng;
   if (!n) return;
-  if (G)
+  if (lane && !G)
+    hipLaunchKernelGGL(k_group_check_lane, grid_for(n), dim3(WAVE), 0, s, S, F, ng, sel, n, ok);
+  else if (G)
     hipLaunchKernelGGL(k_group_check<false>, dim3(n), dim3(GTW_LANES),
                        exclusive ? exclusive_cu_lds<k_group_check<false>>() : 0, s, S, F, ng, G, sel, ok);
   else

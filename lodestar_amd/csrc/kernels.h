@@ -150,9 +150,10 @@ void launch_group_tree(const PipelineBuffers& b, const uint32_t* f_ranges, uint3
 // check: ok_g = FinalExp(F_g * MillerLoop(-g1, S_g)) == 1
 // (sel: check only the entries sel[0 .. n_sel), verdict q -> ok[q])
 // (G: MillerLoop(-g1, S_g) precomputed by launch_group_sig_miller, W_FP12 SoA stride n_groups; null = computed here)
+// (lane: one lane per check instead of a cooperative workgroup -- the fallback's large launches under load; G null)
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t n_groups, uint8_t* ok, hipStream_t s,
                         const uint32_t* sel = nullptr, uint32_t n_sel = 0, const uint32_t* G = nullptr,
-                        bool exclusive = false);
+                        bool exclusive = false, bool lane = false);
 // lane: one lane per group (pairing.hpp miller_loop) instead of a three-wave cooperative workgroup (merged runs)
 void launch_group_sig_miller(const uint32_t* S, uint32_t n_groups, uint32_t* G, hipStream_t s, bool exclusive = false,
                              bool lane = false);

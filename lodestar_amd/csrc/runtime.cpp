@@ -118,6 +118,10 @@ struct Slot {
   DevBuf<uint32_t> d_fkeep;  // the batch pass's per-set Miller values, kept for the fallback (run_shard keep_f)
   HostBuf<uint8_t> h_in, h_res, h_ok;
   HostBuf<uint32_t> h_list;
+  // The slot's own stream for the fallback of its runs (lowest priority).  A failed group's checks used to run on the
+  // run's signature stream, shared by every run of that stream pair: under load (C5, 1% invalid) a 3,424-check launch
+  // held that stream 33-46 ms and the next runs' decodes and MSMs queued behind it (r05 trace).
+  hipStream_t fb = nullptr;
   bool retire = false;     // set under the device queue lock: the dispatcher exits instead of taking work
   bool in_flight = false;  // the slot's run counts in Device::runs_inflight
   bool alone = false;      // no other run was in flight when the slot took its run
@@ -178,6 +182,7 @@ struct Device {
   std::vector<std::thread> workers;
   int runs_inflight = 0;  // under q_mu: runs taken by a slot whose batch pass has not completed
   std::atomic<uint32_t> run_seq{0};  // run counter: the stream pair of a run (BLSGPU_STREAM_PAIRS)
+  std::atomic<int64_t> load{0};  // cost (sets + pubkeys / 256, x256) of the shards queued or running here (routing)
 };
 
 // Device-failure injection (blsgpu_debug_inject, tests only): the next `count` pipeline runs after `skip` more fail as
@@ -211,6 +216,8 @@ struct Options {  // snapshot taken at the start of each call
   int64_t coop_g2_max = 4096;     // runs of <= this many sets take the cooperative [|z|] chains (clearing, subgroup)
   int64_t coop_excl_max = 512;    // cooperative workgroups take a CU each only in runs of <= this many items
   int64_t rsig_spec = 1;          // small idle runs form every r_i sig_i beside the batch pass (for the fallback)
+  int64_t fb_lane_min = 256;      // fallback check launches of >= this many checks take one lane per check (0 = never)
+  int64_t route_split_sets = 16384;  // a call is split over min(devices, sets / this) devices, else routed whole
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
            group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&
@@ -218,7 +225,8 @@ struct Options {  // snapshot taken at the start of each call
            lane_tail_parts == o.lane_tail_parts &&
            msm_slice_mid == o.msm_slice_mid && msm_tree == o.msm_tree &&
            lines_lanes == o.lines_lanes && merge_balance == o.merge_balance && coop_max == o.coop_max &&
-           coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec;
+           coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec &&
+           fb_lane_min == o.fb_lane_min;
   }
 };
 
@@ -283,6 +291,8 @@ inline void add_slices(std::vector<uint32_t>& slices, std::vector<uint32_t>& ran
 struct Shard {
   uint32_t job_begin, job_end;  // job range
   uint32_t set_begin, set_end;  // set range
+  uint32_t dev = 0;             // device index (routing)
+  int64_t cost = 0;             // routing cost, x256 (Device::load)
 };
 
 // Inputs owned by an asynchronous call (the caller may reuse its buffers once blsgpu_submit returns)
@@ -331,6 +341,7 @@ struct blsgpu_ctx {
   int64_t hw_queues = 4;
   std::mutex slots_mu;  // slot creation / resizing
   bool slots_started = false;
+  std::atomic<uint32_t> route_seq{0};  // rotating tie-break of route_rule
 };
 
 namespace {
@@ -361,6 +372,28 @@ void shard_rule(const uint32_t* jfs, const uint32_t* spf, uint32_t n_jobs, uint3
     out[k + 1] = j1;
     j0 = j1;
   }
+}
+
+// ---- routing calls over devices (the rule lodestar_amd/shard.py route_call restates) ---------------------------
+// A call is split over k = min(devices, max(1, n_sets / split_sets)) devices and otherwise routed WHOLE: a gossip
+// call (<= 16k sets at the default) runs on one device at the latency of its full size instead of becoming 2k-set
+// shards on 8 devices (mid-size runs, each no faster than the whole call), while an epoch-scale call (C4: 32,768 sets)
+// still splits.  The k devices are the least loaded (queued + running cost); ties go by distance from the rotating
+// `start`, so equal loads spread.  out[0 .. k) = device indices in shard order; returns k.
+uint32_t route_rule(uint32_t n_sets, uint32_t n_dev, const int64_t* load, int64_t split_sets, uint32_t start,
+                    uint32_t* out) {
+  if (n_dev == 0) return 0;
+  const uint64_t per = (uint64_t)std::max<int64_t>(1, split_sets);
+  const uint32_t k = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_dev, n_sets / per));
+  std::vector<uint32_t> order(n_dev);
+  for (uint32_t d = 0; d < n_dev; d++) order[d] = d;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    if (load[a] != load[b]) return load[a] < load[b];
+    return (a + n_dev - start % n_dev) % n_dev < (b + n_dev - start % n_dev) % n_dev;
+  });
+  std::sort(order.begin(), order.begin() + k);  // shard order = device order (contiguous job ranges)
+  for (uint32_t i = 0; i < k; i++) out[i] = order[i];
+  return k;
 }
 
 // ---- message deduplication: open addressing on the 32-byte signing roots ----------------------------------
@@ -987,7 +1020,10 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     // 8-12 KB/lane of scratch, which the per-queue scratch reservation does not always get.
     constexpr uint32_t kFbLaneMin = 128;
     const uint32_t nr = (uint32_t)retry.size();
-    sl.set_stream(stl);  // the fallback runs on the tail stream, its buffers grow there
+    // the fallback runs on the slot's own stream (the batch pass is complete: sl.done was waited for), its buffers grow
+    // there
+    const hipStream_t sfb = sl.fb ? sl.fb : stl;
+    sl.set_stream(sfb);
     std::vector<uint32_t> rfirst{0}, ritems, rr(2 * (size_t)nr), rf(2 * (size_t)nr), rsl, rrs{0}, rset;
     for (uint32_t q = 0; q < nr; q++) {
       const auto js = job_sets(retry[q]);
@@ -1008,10 +1044,16 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     const bool small_jobs = rsig_spec || rset.size() < (size_t)32 * nr;
     // A small run (cooperative forms: the chip is far from full) checks every retried job directly in ONE launch --
     // up to kFbDirectMax checks run side by side (4 cooperative workgroups per CU) -- instead of sub-groups, a host
-    // round trip and then the jobs of the failing sub-groups: one check round instead of two.
-    constexpr uint32_t kFbDirectMax = 1024;
+    // round trip and then the jobs of the failing sub-groups: one check round instead of two.  (Cooperative checks slow
+    // down with their number -- 96 in 3.1 ms, 257 in 5.7, 675 in 8.1, 1,024 in 16 ms: profiles/r05_fallback_* -- so
+    // beyond ~640 jobs two rounds of few checks are faster; C5's 514 retried jobs: p50 14.7 ms direct, 16.6 in two
+    // rounds.)
+    constexpr uint32_t kFbDirectMax = 640;
     const bool direct = coop && nr <= kFbDirectMax;
     const uint32_t nsub = !direct && nr >= 2 * kFbSub ? (nr + kFbSub - 1) / kFbSub : 0;
+    // Large runs (not cooperative: merged or large calls, throughput first) take lane-per-check launches of many checks;
+    // small runs keep the cooperative checks' latency.
+    auto lane_checks = [&](uint32_t count) { return !coop && opt.fb_lane_min > 0 && count >= (uint32_t)opt.fb_lane_min; };
     std::vector<uint32_t> subr(2 * (size_t)nsub);
     for (uint32_t t = 0; t < nsub; t++) {
       subr[2 * t] = t * kFbSub;
@@ -1041,7 +1083,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     uint32_t* const dF = sl.d_F.p;
     uint32_t* const dS_sub = sl.d_S.p + (size_t)W_G2J * nr;
     uint32_t* const dF_sub = sl.d_F.p + (size_t)W_FP12 * nr;
-    HIPCHK(hipMemcpyAsync(sl.d_list.p, hl, o_sel * 4, hipMemcpyHostToDevice, stl));
+    HIPCHK(hipMemcpyAsync(sl.d_list.p, hl, o_sel * 4, hipMemcpyHostToDevice, sfb));
     PipelineBuffers pr = pb;
     pr.n_chunks = nc;
     pr.chunk_first = sl.d_list.p + 4 * (size_t)nr;
@@ -1051,9 +1093,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     } else {
       st.fallback_miller += (uint32_t)ritems.size();
       if (coop)  // no stored lines in a cooperative run: the per-job chunks hold one set each (mk = 1)
-        launch_miller_coop(pr, false, stl);
+        launch_miller_coop(pr, false, sfb);
       else
-        launch_miller_acc_auto(pr, false, stl, mk, opt.miller_lanes);
+        launch_miller_acc_auto(pr, false, sfb, mk, opt.miller_lanes);
     }
     st.fallback_jobs += nr;
     if (small_jobs) {
@@ -1062,24 +1104,25 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       if (!rsig_spec) sl.d_fb.ensure((size_t)stride * 9 * W_G2J);
       pr.rsig = sl.d_fb.p;
       pr.scal_tab = sl.d_fb.p + (size_t)stride * W_G2J;
-      if (!rsig_spec) launch_sig_scale(pr, (uint32_t)rset.size(), stl, sl.d_list.p + o_rset);
-      launch_group_reduce_lane(pr, sl.d_list.p, sl.d_list.p + 2 * (size_t)nr, nr, dS, dF, stl);
+      if (!rsig_spec) launch_sig_scale(pr, (uint32_t)rset.size(), sfb, sl.d_list.p + o_rset);
+      launch_group_reduce_lane(pr, sl.d_list.p, sl.d_list.p + 2 * (size_t)nr, nr, dS, dF, sfb);
     } else {
       sl.d_msmB.ensure((size_t)MSM_BUCKET_WORDS * std::max<uint32_t>(nrs, 1));
       sl.d_msmW.ensure((size_t)MSM_WINDOW_WORDS * nr);
-      launch_sig_msm(pr, sl.d_list.p + o_rsl, nrs, sl.d_list.p + o_rrs, nr, sl.d_msmB.p, sl.d_msmW.p, dS, stl);
-      launch_group_reduce(pr, sl.d_list.p + 2 * (size_t)nr, nr, dF, stl);
+      launch_sig_msm(pr, sl.d_list.p + o_rsl, nrs, sl.d_list.p + o_rrs, nr, sl.d_msmB.p, sl.d_msmW.p, dS, sfb);
+      launch_group_reduce(pr, sl.d_list.p + 2 * (size_t)nr, nr, dF, sfb);
     }
     std::vector<uint32_t> sel;  // jobs to check on their own
     if (nsub) {
       if (nsub >= kFbLaneMin)
-        launch_range_combine_lane(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, stl);
+        launch_range_combine_lane(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, sfb);
       else
-        launch_range_combine(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, stl);
-      launch_group_check(dS_sub, dF_sub, nsub, sl.d_ok.p + nr, stl);
+        launch_range_combine(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, sfb);
+      launch_group_check(dS_sub, dF_sub, nsub, sl.d_ok.p + nr, sfb, nullptr, 0, nullptr, false,
+                         lane_checks(nsub));
       HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(sl.h_ok.p + nr, sl.d_ok.p + nr, nsub, hipMemcpyDeviceToHost, stl));
-      HIPCHK(hipEventRecord(sl.done, stl));
+      HIPCHK(hipMemcpyAsync(sl.h_ok.p + nr, sl.d_ok.p + nr, nsub, hipMemcpyDeviceToHost, sfb));
+      HIPCHK(hipEventRecord(sl.done, sfb));
       HIPCHK(hipEventSynchronize(sl.done));
       for (uint32_t t = 0; t < nsub; t++)
         for (uint32_t q = subr[2 * t]; q < subr[2 * t + 1]; q++) {
@@ -1092,11 +1135,12 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     if (!sel.empty()) {
       const uint32_t ns = (uint32_t)sel.size();
       memcpy(hl + o_sel, sel.data(), (size_t)ns * 4);
-      HIPCHK(hipMemcpyAsync(sl.d_list.p + o_sel, hl + o_sel, (size_t)ns * 4, hipMemcpyHostToDevice, stl));
-      launch_group_check(dS, dF, nr, sl.d_ok.p, stl, sl.d_list.p + o_sel, ns);
+      HIPCHK(hipMemcpyAsync(sl.d_list.p + o_sel, hl + o_sel, (size_t)ns * 4, hipMemcpyHostToDevice, sfb));
+      launch_group_check(dS, dF, nr, sl.d_ok.p, sfb, sl.d_list.p + o_sel, ns, nullptr, false,
+                         lane_checks(ns));
       HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, ns, hipMemcpyDeviceToHost, stl));
-      HIPCHK(hipEventRecord(sl.done, stl));
+      HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, ns, hipMemcpyDeviceToHost, sfb));
+      HIPCHK(hipEventRecord(sl.done, sfb));
       HIPCHK(hipEventSynchronize(sl.done));
       for (uint32_t k = 0; k < ns; k++) jr[retry[sel[k]]] = sl.h_ok.p[k] ? 1 : 0;
     }
@@ -1474,6 +1518,7 @@ void run_task(Device& d, Slot& sl, const Task& t) {
   if (rc == BLSGPU_DEVICE_ERROR)  // a device failure rejects every job of the shard, never `false`
     for (uint32_t j = sh.job_begin; j < sh.job_end; j++) c->job_result[j] = -BLSGPU_DEVICE_ERROR;
   c->rc[t.shard] = rc;
+  d.load.fetch_sub(sh.cost, std::memory_order_relaxed);
   if (c->remaining.fetch_sub(1) == 1) finish_call(c);
 }
 
@@ -1575,6 +1620,7 @@ void worker_loop(Device* d, Slot* sl) {
     for (size_t p = 0; p < parts.size(); p++) {
       Call* c = parts[p].call;
       c->rc[parts[p].shard] = rcs[p];
+      d->load.fetch_sub(c->shards[parts[p].shard].cost, std::memory_order_relaxed);
       if (c->remaining.fetch_sub(1) == 1) finish_call(c);
     }
   }
@@ -1592,6 +1638,7 @@ void free_slot(Device* d, Slot* s) {
   for (hipEvent_t e : {s->join_in, s->join_msg, s->join_pk, s->join_mask, s->join_gsm, s->join_dec, s->join_msm,
                        s->join_rsig, s->done})
     if (e) (void)hipEventDestroy(e);
+  if (s->fb) (void)hipStreamSynchronize(s->fb), (void)hipStreamDestroy(s->fb);
   delete s;
 }
 
@@ -1604,6 +1651,9 @@ void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet sh
                           &s->join_rsig, &s->done})
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
+    int prio_lo = 0, prio_hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIPCHK(hipStreamCreateWithPriority(&s->fb, hipStreamNonBlocking, prio_lo));
   } catch (HipError&) {
     free_slot(d, s);
     throw;
@@ -1685,22 +1735,37 @@ int ensure_slots(blsgpu_ctx* ctx) {
   return BLSGPU_OK;
 }
 
-// Shards a call over the devices and queues the shard tasks.
+// Routes a call (whole, or split over the least-loaded devices: route_rule) and queues the shard tasks.
+int64_t shard_cost(const blsgpu_batch& b, const Shard& sh) {
+  int64_t c = 256 * (int64_t)(sh.set_end - sh.set_begin);
+  if (b.set_pk_first) c += b.set_pk_first[sh.set_end] - b.set_pk_first[sh.set_begin];
+  return c;
+}
+
 void launch_call(blsgpu_ctx* ctx, Call* c) {
   const blsgpu_batch& b = c->b;
   const uint32_t nd_all = (uint32_t)std::min<int64_t>((int64_t)ctx->devs.size(), c->opt.max_devices);
-  const uint32_t nd = std::max<uint32_t>(1, std::min<uint32_t>(nd_all, (b.n_sets + 255) / 256));
+  std::vector<int64_t> load(nd_all);
+  for (uint32_t d = 0; d < nd_all; d++) load[d] = ctx->devs[d]->load.load(std::memory_order_relaxed);
+  std::vector<uint32_t> devs(std::max<uint32_t>(nd_all, 1));
+  const uint32_t nd = route_rule(b.n_sets, nd_all, load.data(), c->opt.route_split_sets,
+                                 ctx->route_seq.fetch_add(1, std::memory_order_relaxed), devs.data());
   std::vector<uint32_t> parts(nd + 1);
   shard_rule(b.job_first_set, b.set_pk_first, b.n_jobs, nd, parts.data());
-  for (uint32_t k = 0; k < nd; k++)
-    c->shards.push_back({parts[k], parts[k + 1], b.n_jobs ? b.job_first_set[parts[k]] : 0,
-                         b.n_jobs ? b.job_first_set[parts[k + 1]] : 0});
+  for (uint32_t k = 0; k < nd; k++) {
+    Shard sh{parts[k], parts[k + 1], b.n_jobs ? b.job_first_set[parts[k]] : 0,
+             b.n_jobs ? b.job_first_set[parts[k + 1]] : 0};
+    sh.dev = devs[k];
+    sh.cost = shard_cost(b, sh);
+    c->shards.push_back(sh);
+  }
   c->sst.assign(nd, blsgpu_stats{});
   c->rc.assign(nd, BLSGPU_OK);
   c->remaining = nd;
   c->t0 = std::chrono::steady_clock::now();
   for (uint32_t k = 0; k < nd; k++) {
-    Device* d = ctx->devs[k];
+    Device* d = ctx->devs[c->shards[k].dev];
+    d->load.fetch_add(c->shards[k].cost, std::memory_order_relaxed);
     {
       std::lock_guard<std::mutex> lk(d->q_mu);
       d->queue.push_back({c, k});
@@ -1948,6 +2013,12 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
     ctx->opt.coop_excl_max = value;
   } else if (k == "rsig_spec") {
     ctx->opt.rsig_spec = value != 0;
+  } else if (k == "fb_lane_min") {
+    if (value < 0) return BLSGPU_ERR_ARGS;
+    ctx->opt.fb_lane_min = value;
+  } else if (k == "route_split_sets") {
+    if (value < 1) return BLSGPU_ERR_ARGS;
+    ctx->opt.route_split_sets = value;
   } else if (k == "lane_tail_parts") {
     if (value < 0 || value > 3) return BLSGPU_ERR_ARGS;
     ctx->opt.lane_tail_parts = value;
@@ -2010,6 +2081,8 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "coop_g2_max") *value = o.coop_g2_max;
   else if (k == "coop_excl_max") *value = o.coop_excl_max;
   else if (k == "rsig_spec") *value = o.rsig_spec;
+  else if (k == "fb_lane_min") *value = o.fb_lane_min;
+  else if (k == "route_split_sets") *value = o.route_split_sets;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }
@@ -2160,6 +2233,13 @@ int blsgpu_debug_inject(int what, int64_t skip, int64_t count) {
   } else {
     return BLSGPU_ERR_ARGS;
   }
+  return BLSGPU_OK;
+}
+
+int blsgpu_route_call(uint32_t n_sets, uint32_t n_devices, const int64_t* device_load, int64_t split_sets,
+                      uint32_t start, uint32_t* out_devices, uint32_t* n_out) {
+  if (!n_out || n_devices == 0 || !device_load || !out_devices || split_sets < 1) return BLSGPU_ERR_ARGS;
+  *n_out = route_rule(n_sets, n_devices, device_load, split_sets, start, out_devices);
   return BLSGPU_OK;
 }
 

@@ -45,6 +45,7 @@ EXPORTED_SYMBOLS = [
     "blsgpu_chunkify",
     "blsgpu_batch_scalars",
     "blsgpu_debug_inject",
+    "blsgpu_route_call",
 ]
 ROOT_OBJECT = 0
 ROOT_ATTESTATION_DATA = 1
@@ -142,6 +143,8 @@ def load():
     lib.blsgpu_batch_scalars.restype = ctypes.c_int
     lib.blsgpu_debug_inject.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
     lib.blsgpu_debug_inject.restype = ctypes.c_int
+    lib.blsgpu_route_call.argtypes = [u32, u32, vp, ctypes.c_int64, u32, vp, vp]
+    lib.blsgpu_route_call.restype = ctypes.c_int
     _lib = lib
     return lib
 
@@ -161,6 +164,19 @@ def shard_jobs(job_first_set, n_parts, set_pk_first=None):
     if rc != OK:
         raise ValueError(f"blsgpu_shard_jobs -> {code_name(rc)}")
     return [(int(out[k]), int(out[k + 1])) for k in range(n_parts)]
+
+
+def route_call(n_sets, device_load, split_sets=16384, start=0):
+    """The runtime's call routing (C-ABI blsgpu_route_call, pure host code): the devices, in shard order, a call of
+    n_sets sets runs on given each device's queued cost."""
+    dl = np.ascontiguousarray(device_load, dtype=np.int64)
+    out = np.zeros(max(len(dl), 1), np.uint32)
+    k = ctypes.c_uint32(0)
+    rc = load().blsgpu_route_call(n_sets, len(dl), dl.ctypes.data, split_sets, start, out.ctypes.data,
+                                  ctypes.addressof(k))
+    if rc != OK:
+        raise ValueError(f"blsgpu_route_call -> {code_name(rc)}")
+    return [int(x) for x in out[: k.value]]
 
 
 def chunkify(length, min_per_chunk):

@@ -37,6 +37,18 @@ def shard_jobs(job_first_set, n_shards, set_pk_first=None):
     return out
 
 
+def route_call(n_sets, device_load, split_sets=16384, start=0):
+    """Which devices a call runs on (the runtime's route_rule, runtime.cpp; C-ABI blsgpu_route_call): k =
+    min(devices, max(1, n_sets // split_sets)) -- a call below 2 x split_sets sets runs WHOLE on one device -- chosen
+    as the k least loaded, ties broken by distance from `start`, returned in ascending order (shard order)."""
+    n = len(device_load)
+    if n == 0:
+        return []
+    k = max(1, min(n, n_sets // max(1, split_sets)))
+    order = sorted(range(n), key=lambda d: (device_load[d], (d - start) % n))
+    return sorted(order[:k])
+
+
 def max_over_ranks(dt, dist=None):
     """The bench's timing rule: the slowest rank's wall time (gloo all_reduce MAX; control plane only)."""
     if dist is None:

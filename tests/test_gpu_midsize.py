@@ -86,6 +86,7 @@ def test_midsize_one_percent_corrupt_vs_oracle(ctx, pool, n):
     {"coop_max": 1 << 20, "coop_g2_max": 1 << 20},  # cooperative forms everywhere
     {"rsig_spec": 0},                               # the fallback forms r_i sig_i itself
     {"coop_excl_max": 1 << 20},                     # exclusive CUs for every cooperative launch
+    {"fb_lane_min": 1, "coop_max": 0},              # lane-per-check fallback checks (merged runs under load)
 ])
 def test_midsize_forms_agree(ctx, pool, opts):
     saved = {k: ctx.get_option(k) for k in opts}
@@ -141,3 +142,31 @@ def test_mainnet_g2_corpus_in_pipeline(ctx, pool):
             assert (got == 0).all()
     finally:
         ctx.set_option("coop_g2_max", saved)
+
+
+def test_routing_whole_calls_and_split_epoch_calls(pool):
+    """Calls are routed, not sharded (runtime route_rule): on two device contexts a 16k gossip call runs whole on one
+    device, a 32,768-set call (C4's step) splits over both, and concurrent whole calls spread over the devices."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from lodestar_amd.native import Context
+
+    sks, msgs, sigs, pks = pool
+    c2 = Context([0, 0])
+    try:
+        for reps, want_dev in ((2, 1), (4, 2)):
+            n = N_MAX * reps
+            call = dict(job_first_set=np.arange(n + 1, dtype=np.uint32), sigs=sigs * reps,
+                        sig_len=np.full(n, 96, np.uint32), msgs=b"".join(msgs) * reps, pk_bytes=pks * reps,
+                        job_flags=np.ones(n, np.uint8), sig_stride=96)
+            got, st = c2.verify_raw(**call)
+            assert (got == 1).all() and st.devices_used == want_dev, (n, st.devices_used)
+        n = 2048
+        call = dict(job_first_set=np.arange(n + 1, dtype=np.uint32), sigs=sigs[: 96 * n],
+                    sig_len=np.full(n, 96, np.uint32), msgs=b"".join(msgs[:n]), pk_bytes=pks[: 96 * n],
+                    job_flags=np.ones(n, np.uint8), sig_stride=96)
+        with ThreadPoolExecutor(4) as ex:
+            outs = list(ex.map(lambda _: c2.verify_raw(**call), range(8)))
+        assert all((g == 1).all() and st.devices_used == 1 for g, st in outs)
+    finally:
+        c2.close()

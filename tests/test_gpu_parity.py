@@ -324,6 +324,7 @@ def test_two_shards_match_one():
                  job_flags=np.ones(n), sig_stride=192)
     c2 = Context([0, 0])
     try:
+        c2.set_option("route_split_sets", 1024)  # 2,048 sets would otherwise run whole on one device
         got, st = c2.verify_raw(**batch)
         assert st.devices_used == 2
     finally:

@@ -1,0 +1,18 @@
+# usage: bash tools/gpurun/r05_f.sh TAG -- tests (mid-size, configs, faults), C5 under load over slots x lane checks,
+# isolated C5 trace, C2 default
+set -e
+TAG=$1; shift
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_midsize.py tests/test_gpu_configs.py tests/test_gpu_faults.py -x -v --timeout 250 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
+i=0
+for V in "--slots 3" "--slots 3 --set fb_lane_min=0" "--slots 4" "--slots 6"; do
+  i=$((i+1))
+  echo "$V" > gpurun_out/${TAG}_C5_v$i.args
+  timeout -k 10 200 python -u bench.py --config C5 --inflight 32 --steps 300 --warmup 32 --no-cpu-baseline --no-parity $V > gpurun_out/${TAG}_C5_v$i.json 2> gpurun_out/${TAG}_C5_v$i.err
+done
+timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-parity > gpurun_out/${TAG}_C2.json 2> gpurun_out/${TAG}_C2.err
+R=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_load -o run -- \
+  python3 $R/bench.py --config C5 --inflight 32 --steps 200 --warmup 32 --no-cpu-baseline --no-parity > $R/gpurun_out/${TAG}_load.log 2>&1
