@@ -319,6 +319,117 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc2(PipelineBuffers b) {
   st_fp2(b.f_chunk, b.n, c, (6 * (int)h + 4) * W_FP, out.c2);
 }
 
+// Mid-size runs (latency): SIX lanes per pairing, lane k of a group holding the w-basis coefficient f_k of
+// f = sum_k f_k w^k (w^6 = xi; tower slots c0.c0, c1.c0, c0.c1, c1.c1, c0.c2, c1.c2), ten groups per wave.  Every lane
+// runs ONE instruction stream (no divergence inside a group): per step
+//   square:  g_k = sum over i + j = k (mod 6) of f_i f_j (xi where i + j >= 6) -- 21 Fp2 products spread as 4 product
+//            slots per lane (lane-dependent operands from a packed table, one operand doubled for the cross terms, the
+//            xi twist applied by selects inside the lazily reduced recombination; the odd lanes' 4th slot is empty);
+//   line:    h_k = g_k L0 + g_{k-2} L2 + g_{k-3} L3 (xi where the index wraps), L2 = c1 xP, L3 = c4 yP formed one Fp
+//            product per lane (lanes 0-3) and gathered;
+// operands move between the lanes of a group by ds_bpermute (__shfl).  ~7 Fp2 products per lane per doubling step
+// against 14 in the two-lane form: the accumulation of a 2k-16k-pairing run (one wave per SIMD, 10,922 pairings per
+// 1,024 waves) in about half the two-lane time, at ~1.7x the one-lane form's total work.
+#define ACC6_GROUPS (WAVE / 6)
+// squaring slots: nibble k of each word = lane k's operand index i / j; bit k of the masks: doubled, twisted, empty
+__device__ __constant__ const uint32_t ACC6_I[4] = {0x000000u, 0x111121u, 0x224332u, 0x050403u};
+__device__ __constant__ const uint32_t ACC6_J[4] = {0x543210u, 0x432155u, 0x325544u, 0x050403u};
+#define ACC6_DBL(s) ((s) == 0 ? 0x3Eu : (s) == 1 ? 0x3Bu : (s) == 2 ? 0x2Fu : 0x00u)
+#define ACC6_TW(s) ((s) == 0 ? 0x00u : (s) == 1 ? 0x03u : (s) == 2 ? 0x0Fu : 0x15u)
+#define ACC6_NIL(s) ((s) == 3 ? 0x2Au : 0x00u)
+
+BLS_INL fp fp_shfl(const fp& x, int src) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = (uint32_t)__shfl((int)x.l[i], src);
+  return r;
+}
+BLS_INL fp2 fp2_shfl(const fp2& x, int src) { return fp2_make(fp_shfl(x.c0, src), fp_shfl(x.c1, src)); }
+BLS_INL fp fp_keep(bool c, const fp& a) { return fp_select(c, a, fp_zero()); }
+
+// WPE: waves per SIMD the kernel is compiled for -- 1 (301 registers, no scratch) for runs whose groups fit one wave
+// per SIMD, 2 (256 registers, 192 B of scratch) above that (r05: 16k calls 12.9 -> 12.4 ms, 4k calls 9.3 -> 10.5 ms)
+template <bool UNITS, int WPE>
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_miller_acc6(PipelineBuffers b) {
+  const uint32_t lane = threadIdx.x, grp = lane / 6, k = lane % 6;
+  const uint32_t c = blockIdx.x * ACC6_GROUPS + grp;
+  if (grp >= ACC6_GROUPS || c >= b.n_chunks) return;  // whole groups leave together
+  const int base = (int)(grp * 6);
+  const uint32_t k0 = b.chunk_first[c], k1 = b.chunk_first[c + 1];
+  fp2 f = k == 0 ? fp2_one() : fp2_zero();
+  const bool tw2 = k < 2, tw3 = k < 3;
+  int bit = 62;
+  bool add_next = false;
+#pragma unroll 1
+  for (int s = 0; s < MILLER_STEPS; s++) {
+    if (!add_next && s != 0) {
+      // g_k = sum_q tw_q(P_q), tw(x0 + x1 u) = (x0 - x1) + (x0 + x1) u, folded slot by slot into a lazily reduced
+      // partial sum (only f and g stay live across the product calls: two waves per SIMD without spills)
+      fp2 g;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int i = (int)((ACC6_I[q] >> (4 * k)) & 15u), j = (int)((ACC6_J[q] >> (4 * k)) & 15u);
+        const bool dbl = (ACC6_DBL(q) >> k) & 1u, nil = (ACC6_NIL(q) >> k) & 1u, tw = (ACC6_TW(q) >> k) & 1u;
+        const fp2 fi = fp2_shfl(f, base + i), fj = fp2_shfl(f, base + j);
+        const fp2 x = fp2_select(nil, fp2_zero(), fp2_select(dbl, fp2_add_nr(fi, fi), fi));
+        const fp2 P = fp2_mul(x, fj);
+        if (q == 0) {
+          g = P;  // slot 0 is never twisted
+        } else {
+          const fp y = fp_keep(tw, P.c1), z = fp_keep(tw, P.c0);
+          g.c0 = fp_lc(T<1>(g.c0), T<1>(P.c0), T<-1>(y));
+          g.c1 = fp_lc(T<1>(g.c1), T<1>(P.c1), T<1>(z));
+        }
+      }
+      f = g;
+    }
+    const uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
+#pragma unroll 1
+    for (uint32_t it = k0; it < k1; it++) {
+      const uint32_t i = b.chunk_items[it];
+      uint32_t m;
+      bool active;
+      if (UNITS) {
+        m = b.unit_msg[i];
+        active = b.unit_ok[i] != 0;
+      } else {
+        m = b.msg_idx[i];
+        active = b.include[i] != 0;
+      }
+      if (!active || (b.mflags[m] & MF_H_INF)) continue;  // the same on every lane of the group
+      const g1a Pa = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
+      // lanes 0-3: c1.c0 xP, c1.c1 xP, c4.c0 yP, c4.c1 yP (lanes 4, 5 repeat lane 3's product, unused)
+      const uint32_t kc = k < 3 ? k : 3;
+      const fp comp = fp_mul(ld_fp(o, b.nm, m, (int)(2 + kc) * W_FP), kc < 2 ? Pa.x : Pa.y);
+      const fp2 L0 = ld_fp2(o, b.nm, m, 0);
+      const fp2 L2 = fp2_make(fp_shfl(comp, base), fp_shfl(comp, base + 1));
+      const fp2 L3 = fp2_make(fp_shfl(comp, base + 2), fp_shfl(comp, base + 3));
+      const fp2 gm2 = fp2_shfl(f, base + (int)((k + 4) % 6)), gm3 = fp2_shfl(f, base + (int)((k + 3) % 6));
+      fp2 h = fp2_mul(f, L0);
+      {
+        const fp2 B = fp2_mul(gm2, L2);
+        h = fp2_make(fp_lc(T<1>(h.c0), T<1>(B.c0), T<-1>(fp_keep(tw2, B.c1))),
+                     fp_lc(T<1>(h.c1), T<1>(B.c1), T<1>(fp_keep(tw2, B.c0))));
+      }
+      {
+        const fp2 C = fp2_mul(gm3, L3);
+        h = fp2_make(fp_lc(T<1>(h.c0), T<1>(C.c0), T<-1>(fp_keep(tw3, C.c1))),
+                     fp_lc(T<1>(h.c1), T<1>(C.c1), T<1>(fp_keep(tw3, C.c0))));
+      }
+      f = h;
+    }
+    if (!add_next) {
+      add_next = (BLS_Z_ABS >> bit) & 1ull;
+      bit--;
+    } else {
+      add_next = false;
+    }
+  }
+  // f_chunk[c] = conj(f): coefficient k -> tower slot (k odd: c1, else c0) . (k / 2), odd coefficients negated
+  const int slot = (k & 1 ? 3 : 0) + (int)(k >> 1);
+  st_fp2(b.f_chunk, b.n, c, slot * 2 * W_FP, (k & 1) ? fp2_neg(f) : f);
+}
+
 // Small runs (latency): one 128-lane workgroup per pairing, the Miller loop as cooperative Fp12 arithmetic
 // (gt_wave.hpp: lines computed on the fly, one Fp product per lane per step) -- the same value as
 // k_miller_lines + k_miller_acc with one item per chunk, in ~1/6 of the time per pairing, at a fraction of the
@@ -375,6 +486,21 @@ void launch_miller_acc2(const PipelineBuffers& b, bool units, hipStream_t s) {
     hipLaunchKernelGGL(k_miller_acc2<true>, grid_for(2 * b.n_chunks), dim3(WAVE), 0, s, b);
   else
     hipLaunchKernelGGL(k_miller_acc2<false>, grid_for(2 * b.n_chunks), dim3(WAVE), 0, s, b);
+}
+// one wave per SIMD while the groups fit in 1,024 waves (256 CUs x 4 SIMDs), else two
+#define ACC6_W1_MAX_CHUNKS (1024 * ACC6_GROUPS)
+void launch_miller_acc6(const PipelineBuffers& b, bool units, hipStream_t s) {
+  if (!b.n_chunks) return;
+  const dim3 grid((b.n_chunks + ACC6_GROUPS - 1) / ACC6_GROUPS);
+  const bool w2 = b.n_chunks > ACC6_W1_MAX_CHUNKS;
+  if (units && w2)
+    hipLaunchKernelGGL((k_miller_acc6<true, 2>), grid, dim3(WAVE), 0, s, b);
+  else if (units)
+    hipLaunchKernelGGL((k_miller_acc6<true, 1>), grid, dim3(WAVE), 0, s, b);
+  else if (w2)
+    hipLaunchKernelGGL((k_miller_acc6<false, 2>), grid, dim3(WAVE), 0, s, b);
+  else
+    hipLaunchKernelGGL((k_miller_acc6<false, 1>), grid, dim3(WAVE), 0, s, b);
 }
 void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s) {
   if (!b.n_chunks) return;

@@ -128,6 +128,8 @@ void launch_miller_lines2(const PipelineBuffers& b, hipStream_t s);
 void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s);
 // the same for chunks of ONE item each, two lanes per pairing (k_miller.hip k_miller_acc2: mid-size runs, latency)
 void launch_miller_acc2(const PipelineBuffers& b, bool units, hipStream_t s);
+// the same on SIX lanes per chunk, one w-basis Fp2 coefficient of f per lane (k_miller_acc6: 2k-16k-pairing runs)
+void launch_miller_acc6(const PipelineBuffers& b, bool units, hipStream_t s);
 // the same for chunks of ONE item each, as one cooperative 128-lane workgroup per pairing (lines on the fly; small
 // runs, for latency)
 // (exclusive: each workgroup takes a CU to itself -- k_common.hpp exclusive_cu_lds -- for latency-bound small runs;

@@ -212,12 +212,15 @@ struct Options {  // snapshot taken at the start of each call
   int64_t lines_lanes = 1;        // lanes per message of the Miller lines (1, 2)
   int64_t merge_balance = 0;      // a backlog above merge_sets is cut into equal runs
   int64_t msm_tree = 1;           // those runs sum each range's slices by a pairwise tree
-  int64_t coop_max = 2048;        // runs of <= this many pairings take the cooperative Miller loops (k_miller_coop)
+  int64_t coop_max = 512;         // runs of <= this many pairings take the cooperative Miller loops (k_miller_coop)
   int64_t coop_g2_max = 4096;     // runs of <= this many sets take the cooperative [|z|] chains (clearing, subgroup)
   int64_t coop_excl_max = 512;    // cooperative workgroups take a CU each only in runs of <= this many items
   int64_t rsig_spec = 1;          // small idle runs form every r_i sig_i beside the batch pass (for the fallback)
   int64_t fb_lane_min = 256;      // fallback check launches of >= this many checks take one lane per check (0 = never)
   int64_t route_split_sets = 16384;  // a call is split over min(devices, sets / this) devices, else routed whole
+  int64_t acc6_max = 16384;       // one-item-chunk runs of <= this many chunks take the six-lane accumulation
+  int64_t small_max = 4096;       // runs of <= this many sets are latency-first (speculation, cooperative fallback checks)
+  int64_t fb_direct_min = 1024;   // large runs under load with >= this many retried jobs check each directly (0 = never)
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
            group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&
@@ -226,7 +229,8 @@ struct Options {  // snapshot taken at the start of each call
            msm_slice_mid == o.msm_slice_mid && msm_tree == o.msm_tree &&
            lines_lanes == o.lines_lanes && merge_balance == o.merge_balance && coop_max == o.coop_max &&
            coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec &&
-           fb_lane_min == o.fb_lane_min;
+           fb_lane_min == o.fb_lane_min && acc6_max == o.acc6_max && small_max == o.small_max &&
+           fb_direct_min == o.fb_direct_min;
   }
 };
 
@@ -255,9 +259,15 @@ inline uint32_t miller_k_auto(uint32_t n_items) {
   return k;
 }
 
-// The Miller accumulation of a run's chunks: two lanes per pairing (k_miller_acc2) when the chunks hold one item each
-// and one lane per chunk would leave SIMDs idle (< 65,536 chunks = 1,024 waves), else one lane per chunk.
-void launch_miller_acc_auto(const PipelineBuffers& pb, bool units, hipStream_t st, uint32_t mk, int64_t lanes_opt) {
+// The Miller accumulation of a run's chunks: six lanes per chunk (k_miller_acc6) for runs of one-item chunks up to
+// acc6_max chunks, two lanes (k_miller_acc2) for larger one-item-chunk runs while one lane per chunk would leave SIMDs
+// idle (< 65,536 chunks = 1,024 waves), else one lane per chunk.
+void launch_miller_acc_auto(const PipelineBuffers& pb, bool units, hipStream_t st, uint32_t mk, int64_t lanes_opt,
+                            int64_t acc6_max) {
+  if (lanes_opt == 6 || (lanes_opt == 0 && mk == 1 && (int64_t)pb.n_chunks <= acc6_max)) {
+    launch_miller_acc6(pb, units, st);
+    return;
+  }
   // two lanes per chunk: f never on one lane, no spills (r4zd/r4ze A/B, PMC r4f); auto: one-item chunks
   const bool two = lanes_opt == 2 || (lanes_opt == 0 && mk == 1);
   if (two)
@@ -581,7 +591,11 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // failed group's per-job checks need.  They are copied aside before the F tree multiplies chunks in place, and the
   // fallback takes F_j = prod of its sets' kept values instead of re-running the Miller loops.
   const bool keep_f = !merged && mk == 1 && n_chunks == n;
-  const bool spec = BLSGPU_STREAM_PAIRS && coop && sl.alone && !opt.serial;  // speculative MSM (kernel pipeline below)
+  // A small run (<= opt.small_max sets) leaves most of the chip idle whatever its kernel forms: on an idle device it takes
+  // the other stream pair too (speculative MSM, parallel pubkey branch, r_i sig_i), and its fallback checks stay
+  // cooperative (latency) instead of lane-per-check (throughput).
+  const bool small = n <= (uint32_t)opt.small_max;
+  const bool spec = BLSGPU_STREAM_PAIRS && small && sl.alone && !opt.serial;  // speculative MSM (kernel pipeline below)
   // A small run on an idle device also forms every r_i sig_i (k_sig_scale) on the idle pubkey stream once its pubkeys
   // and the decode are done: the chip has room, and a failed group's per-job checks then start from the sums instead
   // of a 1.7 ms scaling launch on the fallback's critical path (the batch pass itself never reads them).
@@ -604,7 +618,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     add_slices(slices, range_slices, job_sets(group_jobs[g].first).first, job_sets(group_jobs[g].second - 1).second,
                slice_len);
   const uint32_t n_slices = (uint32_t)(slices.size() / 2);
-  if (n > kMsmSmallSliceMaxSets && n <= kMsmHalfSliceMaxSets && opt.msm_tree) {
+  // (runs of <= 1,024 sets too: a 1,024-set call's 32 slices summed serially by the window lanes took 2.0 ms beside the
+  // cooperative Miller loops and made the signature branch its critical path -- r05 trace)
+  if (n <= kMsmHalfSliceMaxSets && opt.msm_tree) {
     for (uint32_t g = 0; g < ng0; g++) msm_tree = std::max(msm_tree, range_slices[g + 1] - range_slices[g]);
     // the tree's launches are sized n_ranges x (most slices of a range): only when the ranges are about equal (one
     // large job beside many single-set groups would launch ~n_ranges x max_pairs idle lanes per level)
@@ -809,7 +825,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // its own signature decode and subgroup checks instead of in front of them: the signature branch was a small
   // call's critical path (C1 serial trace: 7.25 ms vs the message branch's 6.15).
   hipStream_t sm = BLSGPU_STREAM_PAIRS ? d.st[2 * par + 1] : d.st[kMsg],
-              sp = BLSGPU_STREAM_PAIRS ? (coop && sl.alone ? d.st[2 * (1 - par)] : s) : d.st[kPk],
+              sp = BLSGPU_STREAM_PAIRS ? (small && sl.alone ? d.st[2 * (1 - par)] : s) : d.st[kPk],
               stl = BLSGPU_STREAM_PAIRS ? s : d.st[kTail];
   if (opt.serial) sm = sp = stl = s;
   auto beg = [&](int k, hipStream_t st) {
@@ -891,7 +907,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     if (coop)
       launch_miller_coop(pb, merged, sm, excl);
     else
-      launch_miller_acc_auto(pb, merged, sm, mk, opt.miller_lanes);
+      launch_miller_acc_auto(pb, merged, sm, mk, opt.miller_lanes, opt.acc6_max);
     end(5, sm);
     if (keep_f)
       HIPCHK(hipMemcpyAsync(sl.d_fkeep.p, pb.f_chunk, (size_t)stride * W_FP12 * 4, hipMemcpyDeviceToDevice, sm));
@@ -1049,11 +1065,15 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     // beyond ~640 jobs two rounds of few checks are faster; C5's 514 retried jobs: p50 14.7 ms direct, 16.6 in two
     // rounds.)
     constexpr uint32_t kFbDirectMax = 640;
-    const bool direct = coop && nr <= kFbDirectMax;
+    // Large runs under load (other runs in flight: merged calls, throughput first) take lane-per-check launches of many
+    // checks, and with many retried jobs (>= fb_direct_min: dense failures, e.g. C5's 1% invalid sets fail every
+    // group) check every job directly in ONE lane launch: three times the checks of the sub-group round trip, but one
+    // ~25 ms lane round instead of two, and the run's call latency is what bounds a loaded device's throughput
+    // (calls in flight / latency).  Small runs and runs on an idle device keep the cooperative checks' latency.
+    const bool busy = !small && !sl.alone;
+    auto lane_checks = [&](uint32_t count) { return busy && opt.fb_lane_min > 0 && count >= (uint32_t)opt.fb_lane_min; };
+    const bool direct = (small && nr <= kFbDirectMax) || (busy && opt.fb_direct_min > 0 && nr >= (uint32_t)opt.fb_direct_min);
     const uint32_t nsub = !direct && nr >= 2 * kFbSub ? (nr + kFbSub - 1) / kFbSub : 0;
-    // Large runs (not cooperative: merged or large calls, throughput first) take lane-per-check launches of many checks;
-    // small runs keep the cooperative checks' latency.
-    auto lane_checks = [&](uint32_t count) { return !coop && opt.fb_lane_min > 0 && count >= (uint32_t)opt.fb_lane_min; };
     std::vector<uint32_t> subr(2 * (size_t)nsub);
     for (uint32_t t = 0; t < nsub; t++) {
       subr[2 * t] = t * kFbSub;
@@ -1095,7 +1115,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       if (coop)  // no stored lines in a cooperative run: the per-job chunks hold one set each (mk = 1)
         launch_miller_coop(pr, false, sfb);
       else
-        launch_miller_acc_auto(pr, false, sfb, mk, opt.miller_lanes);
+        launch_miller_acc_auto(pr, false, sfb, mk, opt.miller_lanes, opt.acc6_max);
     }
     st.fallback_jobs += nr;
     if (small_jobs) {
@@ -1990,7 +2010,7 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "serial") {
     ctx->opt.serial = value != 0;
   } else if (k == "miller_lanes") {
-    if (value < 0 || value > 2) return BLSGPU_ERR_ARGS;
+    if (value < 0 || (value > 2 && value != 6)) return BLSGPU_ERR_ARGS;
     ctx->opt.miller_lanes = value;
   } else if (k == "msm_slice_mid") {
     if (value < 8 || value > MSM_SLICE) return BLSGPU_ERR_ARGS;
@@ -2016,6 +2036,15 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "fb_lane_min") {
     if (value < 0) return BLSGPU_ERR_ARGS;
     ctx->opt.fb_lane_min = value;
+  } else if (k == "fb_direct_min") {
+    if (value < 0) return BLSGPU_ERR_ARGS;
+    ctx->opt.fb_direct_min = value;
+  } else if (k == "small_max") {
+    if (value < 0) return BLSGPU_ERR_ARGS;
+    ctx->opt.small_max = value;
+  } else if (k == "acc6_max") {
+    if (value < 0) return BLSGPU_ERR_ARGS;
+    ctx->opt.acc6_max = value;
   } else if (k == "route_split_sets") {
     if (value < 1) return BLSGPU_ERR_ARGS;
     ctx->opt.route_split_sets = value;
@@ -2083,6 +2112,9 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "rsig_spec") *value = o.rsig_spec;
   else if (k == "fb_lane_min") *value = o.fb_lane_min;
   else if (k == "route_split_sets") *value = o.route_split_sets;
+  else if (k == "acc6_max") *value = o.acc6_max;
+  else if (k == "small_max") *value = o.small_max;
+  else if (k == "fb_direct_min") *value = o.fb_direct_min;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }

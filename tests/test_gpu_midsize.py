@@ -87,6 +87,8 @@ def test_midsize_one_percent_corrupt_vs_oracle(ctx, pool, n):
     {"rsig_spec": 0},                               # the fallback forms r_i sig_i itself
     {"coop_excl_max": 1 << 20},                     # exclusive CUs for every cooperative launch
     {"fb_lane_min": 1, "coop_max": 0},              # lane-per-check fallback checks (merged runs under load)
+    {"coop_max": 0, "acc6_max": 0},                 # two-lane accumulation instead of the six-lane one
+    {"coop_max": 0, "miller_lanes": 6, "dedupe": 0},  # six lanes forced
 ])
 def test_midsize_forms_agree(ctx, pool, opts):
     saved = {k: ctx.get_option(k) for k in opts}

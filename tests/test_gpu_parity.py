@@ -413,22 +413,26 @@ def test_merged_run_isolates_bad_call():
         c.close()
 
 
-@pytest.mark.parametrize("k,lanes", [(2, 2), (4, 2), (2, 1), (1, 1)])
+@pytest.mark.parametrize("k,lanes", [(2, 2), (4, 2), (2, 1), (1, 1), (1, 6), (2, 6), (3, 6)])
 def test_miller_chunk_forms_vs_oracle(ctx, k, lanes):
-    """The Miller accumulation's chunk forms: chunks of k pairings on two lanes (halves of f, the squaring shared by
-    the chunk) or one lane, forced on a 2,048-set call with ~1% corrupted sets (so the fallback re-checks jobs
-    through the same kernels): job for job equal to the oracle."""
+    """The Miller accumulation's chunk forms: chunks of k pairings on six lanes (one w-basis coefficient of f each),
+    two lanes (halves of f, the squaring shared by the chunk) or one lane, forced on a 2,048-set call with ~1% corrupted
+    sets (so the fallback re-checks jobs through the same kernels): job for job equal to the oracle.  (coop_max 0: the
+    lane forms even for a run this small.)"""
     n = 2048
     rng = np.random.default_rng(n + 17 * k + lanes)
     sks, pks, msgs, sigs, sig_len = corrupted_single_sets(n, b"MK", rng)
     base = dict(sigs=sigs, sig_len=sig_len, msgs=b"".join(msgs), sig_stride=192)
+    coop = ctx.get_option("coop_max")
     ctx.set_option("miller_k", k)
     ctx.set_option("miller_lanes", lanes)
+    ctx.set_option("coop_max", 0)
     try:
         got, st = compare(ctx, job_first_set=np.arange(n + 1), pk_bytes=pks, job_flags=np.ones(n), **base)
     finally:
         ctx.set_option("miller_k", 0)
         ctx.set_option("miller_lanes", 0)
+        ctx.set_option("coop_max", coop)
     assert (got == 1).sum() >= n - max(8, n // 100) and st.batch_retries >= 1
 
 
