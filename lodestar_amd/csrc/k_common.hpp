@@ -147,6 +147,44 @@ BLS_INL fp fp_xlane(const fp& x) {
 }
 BLS_INL fp2 fp2_xlane(const fp2& x) { return fp2_make(fp_xlane(x.c0), fp_xlane(x.c1)); }
 BLS_INL fp6 fp6_xlane(const fp6& x) { return fp6_make(fp2_xlane(x.c0), fp2_xlane(x.c1), fp2_xlane(x.c2)); }
+// The 68 Miller lines of Q (affine, finite) in Q-only form (l0, c1, c4), step s of column u at
+// lines[(s * W_LINE + w) * nm + u] (k_miller_lines: one column per distinct message; k_check_lines: per fallback check)
+__device__ __forceinline__ void miller_lines_store(const g2a& Q, uint32_t* lines, uint32_t nm, uint32_t u) {
+  g2proj T;
+  T.x = Q.x;
+  T.y = Q.y;
+  T.z = fp2_one();
+  int bit = 62;
+  bool add_next = false;
+#pragma unroll 1
+  for (int s = 0; s < MILLER_STEPS; s++) {
+    line3 L;
+    if (!add_next) {
+      miller_dbl_line(T, L);
+      add_next = (BLS_Z_ABS >> bit) & 1ull;
+      bit--;
+    } else {
+      miller_add_line(T, Q, L);
+      add_next = false;
+    }
+    uint32_t* o = lines + (size_t)s * W_LINE * nm;
+    st_fp2(o, nm, u, 0, L.l0);
+    st_fp2(o, nm, u, 2 * W_FP, L.c1);
+    st_fp2(o, nm, u, 4 * W_FP, L.c4);
+  }
+}
+
+// any-lane exchange of register values (ds_bpermute; the lane-group kernels k_miller_acc6 / gt6.hpp)
+BLS_INL fp fp_shfl(const fp& x, int src) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = (uint32_t)__shfl((int)x.l[i], src);
+  return r;
+}
+BLS_INL fp2 fp2_shfl(const fp2& x, int src) { return fp2_make(fp_shfl(x.c0, src), fp_shfl(x.c1, src)); }
+BLS_INL fp fp_keep(bool c, const fp& a) { return fp_select(c, a, fp_zero()); }
+// lane groups of six (k_miller_acc6, gt6.hpp): ten per wave, lanes 60-63 idle
+#define ACC6_GROUPS (WAVE / 6)
 BLS_INL g2j g2j_xlane(const g2j& p) {
   g2j r;
   r.x = fp2_xlane(p.x);

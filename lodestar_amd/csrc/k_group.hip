@@ -11,6 +11,7 @@
 // (runtime.cpp), so the fallback costs one Miller loop + final exponentiation per tested sub-range.
 #include "k_common.hpp"
 #include "gt_wave.hpp"
+#include "gt6.hpp"
 
 // Lane per job: first error of the job, pubkeys before signatures (the reference deserializes pubkeys
 // first, worker.ts:39 / maybeBatch.ts:23), and the include mask of its sets.
@@ -134,6 +135,33 @@ STAGE_KERNEL_W(BLSGPU_WPE_GRP) void k_group_sig_miller_lane(const uint32_t* S_in
   st_fp12(G_out, ng, g, G);
 }
 
+// Lines of S for the fallback's six-lane checks: lane per entry sel[q] (all ng when sel is null): S -> affine, its 68
+// Miller lines to column sel[q] of `lines` (stride ng); flags[sel[q]] = 1 when S is the identity (no lines).
+STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_check_lines(const uint32_t* S_in, uint32_t ng, const uint32_t* sel, uint32_t n,
+                                                   uint32_t* lines, uint8_t* flags) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  if (q >= n) return;
+  const uint32_t g = sel ? sel[q] : q;
+  g2a Sa;
+  const bool fin = jac_to_aff(ld_g2j(S_in, ng, g), Sa);
+  flags[g] = fin ? 0 : 1;
+  if (fin) miller_lines_store(Sa, lines, ng, g);
+}
+
+// the same for the entries sel[0 .. n) only (G columns sel[q]; the fallback's six-lane checks)
+STAGE_KERNEL_W(BLSGPU_WPE_GRP) void k_group_sig_miller_lane_sel(const uint32_t* S_in, uint32_t ng, const uint32_t* sel,
+                                                               uint32_t n, uint32_t* G_out) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  if (q >= n) return;
+  const uint32_t g = sel ? sel[q] : q;
+  g2a Sa;
+  g1a P;
+  P.x = G1_GEN_X;
+  P.y = G1_NEG_GEN_Y;
+  const fp12 G = jac_to_aff(ld_g2j(S_in, ng, g), Sa) ? miller_loop(P, Sa) : fp12_one();
+  st_fp12(G_out, ng, g, G);
+}
+
 // MILLER: G_in is null, the kernel runs MillerLoop(-g1, S) itself (three waves, gtw_miller_loop); otherwise two
 template <bool MILLER>
 __global__ __launch_bounds__(MILLER ? GTW_MILLER_LANES : GTW_LANES) void k_group_check(
@@ -176,6 +204,31 @@ STAGE_KERNEL_W(BLSGPU_WPE_GRP) void k_group_check_lane(const uint32_t* S_in, con
     F = fp12_mul(F, miller_loop(P, Sa));
   }
   ok[q] = fp12_is_one(final_exponentiation(F)) ? 1 : 0;
+}
+
+// The fallback's checks on SIX lanes per check (gt6.hpp): FinalExp(F * G) == 1 with G = MillerLoop(-g1, S) computed
+// beforehand (k_group_sig_miller_lane) -- the final exponentiation in ~1/6 of the one-lane time, ten checks per wave:
+// for the dense-failure launches of merged runs under load, where a one-lane check's ~25 ms was the run's latency.
+// MILLER: G = MillerLoop(-g1, S) on the same six lanes from S's stored lines (k_check_lines; flags[gi] set: S is the
+// identity, G = 1), else G_in.
+template <bool MILLER>
+STAGE_KERNEL_W(BLSGPU_WPE_GRP) void k_group_check6(const uint32_t* F_in, const uint32_t* G_in, uint32_t ng,
+                                                  const uint32_t* sel, uint32_t n, uint8_t* ok, const uint32_t* lines,
+                                                  const uint8_t* flags) {
+  const uint32_t lane = threadIdx.x, grp = lane / 6, k = lane % 6;
+  const uint32_t q = blockIdx.x * ACC6_GROUPS + grp;
+  if (grp >= ACC6_GROUPS || q >= n) return;  // whole groups leave together
+  const uint32_t gi = sel ? sel[q] : q;
+  const G6 g{(int)(grp * 6), k};
+  const int w0 = ((k & 1) ? 3 : 0) * 2 * W_FP + (int)(k >> 1) * 2 * W_FP;
+  const fp2 F = ld_fp2(F_in, ng, gi, w0);
+  fp2 G;
+  if (MILLER)
+    G = flags[gi] ? (k == 0 ? fp2_one() : fp2_zero()) : g6_miller(lines, ng, gi, G1_GEN_X, G1_NEG_GEN_Y, g);
+  else
+    G = ld_fp2(G_in, ng, gi, w0);
+  const bool one = g6_is_one(g6_final_exp(g6_mul(F, G, g), g), g);
+  if (k == 0) ok[q] = one ? 1 : 0;
 }
 
 // Fallback sub-groups: S_out[r] = sum S_in[e], F_out[r] = prod F_in[e] over the entries e of range r
@@ -273,6 +326,26 @@ void launch_group_tree(const PipelineBuffers& b, const uint32_t* f_ranges, uint3
     p0 = p1;
   }
   hipLaunchKernelGGL(k_f_gather, grid_for(ng * W_FP12), dim3(WAVE), 0, s, b, f_ranges, ng, F);
+}
+void launch_group_sig_miller_sel(const uint32_t* S, uint32_t ng, const uint32_t* sel, uint32_t n_sel, uint32_t* G,
+                                 hipStream_t s) {
+  const uint32_t n = sel ? n_sel : ng;
+  if (n) hipLaunchKernelGGL(k_group_sig_miller_lane_sel, grid_for(n), dim3(WAVE), 0, s, S, ng, sel, n, G);
+}
+void launch_group_check6(const uint32_t* F, const uint32_t* G, uint32_t ng, uint8_t* ok, hipStream_t s,
+                         const uint32_t* sel, uint32_t n_sel) {
+  const uint32_t n = sel ? n_sel : ng;
+  if (n)
+    hipLaunchKernelGGL(k_group_check6<false>, dim3((n + ACC6_GROUPS - 1) / ACC6_GROUPS), dim3(WAVE), 0, s, F, G, ng,
+                       sel, n, ok, nullptr, nullptr);
+}
+void launch_check6_miller(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s,
+                          const uint32_t* sel, uint32_t n_sel, uint32_t* lines, uint8_t* flags) {
+  const uint32_t n = sel ? n_sel : ng;
+  if (!n) return;
+  hipLaunchKernelGGL(k_check_lines, grid_for(n), dim3(WAVE), 0, s, S, ng, sel, n, lines, flags);
+  hipLaunchKernelGGL(k_group_check6<true>, dim3((n + ACC6_GROUPS - 1) / ACC6_GROUPS), dim3(WAVE), 0, s, F, nullptr, ng,
+                     sel, n, ok, lines, flags);
 }
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, hipStream_t s,
                         const uint32_t* sel, uint32_t n_sel, const uint32_t* G, bool exclusive, bool lane) {

@@ -14,6 +14,7 @@
 // Line traffic is 68 x 84 words = 22.8 KB per message (HBM-cheap next to ~5,200 Montgomery products).
 #include "k_common.hpp"
 #include "gt_wave.hpp"
+#include "gt6.hpp"
 
 // Line pairs in the one-lane chunk loop (line_pair + fp12_mul_by_line2: 23 Fp2 products per two items instead of 26):
 // correct (test_line_pair_product, chunk-form GPU parity) but the pending line and the denser product raise the
@@ -34,29 +35,7 @@ BLS_INL fp fp_add_n(const fp& a, const fp& b) { return fp_add_norm(a, b); }
 STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_miller_lines(PipelineBuffers b) {
   uint32_t u = blockIdx.x * WAVE + threadIdx.x;
   if (u >= b.n_umsg || (b.mflags[u] & MF_H_INF)) return;
-  const g2a Q = ld_g2a(b.h_aff, b.nm, u);
-  g2proj T;
-  T.x = Q.x;
-  T.y = Q.y;
-  T.z = fp2_one();
-  int bit = 62;
-  bool add_next = false;
-#pragma unroll 1
-  for (int s = 0; s < MILLER_STEPS; s++) {
-    line3 L;
-    if (!add_next) {
-      miller_dbl_line(T, L);
-      add_next = (BLS_Z_ABS >> bit) & 1ull;
-      bit--;
-    } else {
-      miller_add_line(T, Q, L);
-      add_next = false;
-    }
-    uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
-    st_fp2(o, b.nm, u, 0, L.l0);
-    st_fp2(o, b.nm, u, 2 * W_FP, L.c1);
-    st_fp2(o, b.nm, u, 4 * W_FP, L.c4);
-  }
+  miller_lines_store(ld_g2a(b.h_aff, b.nm, u), b.lines, b.nm, u);
 }
 
 // The same lines on TWO lanes per message (mid-size runs, latency): both lanes hold T; a doubling step's products run
@@ -330,23 +309,6 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc2(PipelineBuffers b) {
 // operands move between the lanes of a group by ds_bpermute (__shfl).  ~7 Fp2 products per lane per doubling step
 // against 14 in the two-lane form: the accumulation of a 2k-16k-pairing run (one wave per SIMD, 10,922 pairings per
 // 1,024 waves) in about half the two-lane time, at ~1.7x the one-lane form's total work.
-#define ACC6_GROUPS (WAVE / 6)
-// squaring slots: nibble k of each word = lane k's operand index i / j; bit k of the masks: doubled, twisted, empty
-__device__ __constant__ const uint32_t ACC6_I[4] = {0x000000u, 0x111121u, 0x224332u, 0x050403u};
-__device__ __constant__ const uint32_t ACC6_J[4] = {0x543210u, 0x432155u, 0x325544u, 0x050403u};
-#define ACC6_DBL(s) ((s) == 0 ? 0x3Eu : (s) == 1 ? 0x3Bu : (s) == 2 ? 0x2Fu : 0x00u)
-#define ACC6_TW(s) ((s) == 0 ? 0x00u : (s) == 1 ? 0x03u : (s) == 2 ? 0x0Fu : 0x15u)
-#define ACC6_NIL(s) ((s) == 3 ? 0x2Au : 0x00u)
-
-BLS_INL fp fp_shfl(const fp& x, int src) {
-  fp r;
-#pragma unroll
-  for (int i = 0; i < BLS_NL; i++) r.l[i] = (uint32_t)__shfl((int)x.l[i], src);
-  return r;
-}
-BLS_INL fp2 fp2_shfl(const fp2& x, int src) { return fp2_make(fp_shfl(x.c0, src), fp_shfl(x.c1, src)); }
-BLS_INL fp fp_keep(bool c, const fp& a) { return fp_select(c, a, fp_zero()); }
-
 // WPE: waves per SIMD the kernel is compiled for -- 1 (301 registers, no scratch) for runs whose groups fit one wave
 // per SIMD, 2 (256 registers, 192 B of scratch) above that (r05: 16k calls 12.9 -> 12.4 ms, 4k calls 9.3 -> 10.5 ms)
 template <bool UNITS, int WPE>
@@ -357,31 +319,12 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE, WPE))
   const int base = (int)(grp * 6);
   const uint32_t k0 = b.chunk_first[c], k1 = b.chunk_first[c + 1];
   fp2 f = k == 0 ? fp2_one() : fp2_zero();
-  const bool tw2 = k < 2, tw3 = k < 3;
   int bit = 62;
   bool add_next = false;
 #pragma unroll 1
   for (int s = 0; s < MILLER_STEPS; s++) {
     if (!add_next && s != 0) {
-      // g_k = sum_q tw_q(P_q), tw(x0 + x1 u) = (x0 - x1) + (x0 + x1) u, folded slot by slot into a lazily reduced
-      // partial sum (only f and g stay live across the product calls: two waves per SIMD without spills)
-      fp2 g;
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int i = (int)((ACC6_I[q] >> (4 * k)) & 15u), j = (int)((ACC6_J[q] >> (4 * k)) & 15u);
-        const bool dbl = (ACC6_DBL(q) >> k) & 1u, nil = (ACC6_NIL(q) >> k) & 1u, tw = (ACC6_TW(q) >> k) & 1u;
-        const fp2 fi = fp2_shfl(f, base + i), fj = fp2_shfl(f, base + j);
-        const fp2 x = fp2_select(nil, fp2_zero(), fp2_select(dbl, fp2_add_nr(fi, fi), fi));
-        const fp2 P = fp2_mul(x, fj);
-        if (q == 0) {
-          g = P;  // slot 0 is never twisted
-        } else {
-          const fp y = fp_keep(tw, P.c1), z = fp_keep(tw, P.c0);
-          g.c0 = fp_lc(T<1>(g.c0), T<1>(P.c0), T<-1>(y));
-          g.c1 = fp_lc(T<1>(g.c1), T<1>(P.c1), T<1>(z));
-        }
-      }
-      f = g;
+      f = g6_sqr(f, G6{base, k});
     }
     const uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
 #pragma unroll 1
@@ -398,25 +341,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE, WPE))
       }
       if (!active || (b.mflags[m] & MF_H_INF)) continue;  // the same on every lane of the group
       const g1a Pa = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
-      // lanes 0-3: c1.c0 xP, c1.c1 xP, c4.c0 yP, c4.c1 yP (lanes 4, 5 repeat lane 3's product, unused)
-      const uint32_t kc = k < 3 ? k : 3;
-      const fp comp = fp_mul(ld_fp(o, b.nm, m, (int)(2 + kc) * W_FP), kc < 2 ? Pa.x : Pa.y);
-      const fp2 L0 = ld_fp2(o, b.nm, m, 0);
-      const fp2 L2 = fp2_make(fp_shfl(comp, base), fp_shfl(comp, base + 1));
-      const fp2 L3 = fp2_make(fp_shfl(comp, base + 2), fp_shfl(comp, base + 3));
-      const fp2 gm2 = fp2_shfl(f, base + (int)((k + 4) % 6)), gm3 = fp2_shfl(f, base + (int)((k + 3) % 6));
-      fp2 h = fp2_mul(f, L0);
-      {
-        const fp2 B = fp2_mul(gm2, L2);
-        h = fp2_make(fp_lc(T<1>(h.c0), T<1>(B.c0), T<-1>(fp_keep(tw2, B.c1))),
-                     fp_lc(T<1>(h.c1), T<1>(B.c1), T<1>(fp_keep(tw2, B.c0))));
-      }
-      {
-        const fp2 C = fp2_mul(gm3, L3);
-        h = fp2_make(fp_lc(T<1>(h.c0), T<1>(C.c0), T<-1>(fp_keep(tw3, C.c1))),
-                     fp_lc(T<1>(h.c1), T<1>(C.c1), T<1>(fp_keep(tw3, C.c0))));
-      }
-      f = h;
+      f = g6_line_mul(f, o, b.nm, m, Pa.x, Pa.y, G6{base, k});
     }
     if (!add_next) {
       add_next = (BLS_Z_ABS >> bit) & 1ull;

@@ -156,6 +156,17 @@ void launch_group_tree(const PipelineBuffers& b, const uint32_t* f_ranges, uint3
 void launch_group_check(const uint32_t* S, const uint32_t* F, uint32_t n_groups, uint8_t* ok, hipStream_t s,
                         const uint32_t* sel = nullptr, uint32_t n_sel = 0, const uint32_t* G = nullptr,
                         bool exclusive = false, bool lane = false);
+// six lanes per check (k_group_check6, gt6.hpp): ok = FinalExp(F * G) == 1 with G = MillerLoop(-g1, S) precomputed
+// (launch_group_sig_miller; sel: check only entries sel[0 .. n_sel), verdict q -> ok[q])
+void launch_group_check6(const uint32_t* F, const uint32_t* G, uint32_t n_groups, uint8_t* ok, hipStream_t s,
+                         const uint32_t* sel = nullptr, uint32_t n_sel = 0);
+// the whole check on six lanes: S's Miller lines one lane per entry (k_check_lines, into `lines`: n_groups x 68 x W_LINE
+// words; flags: n_groups bytes), then MillerLoop(-g1, S), F * G and the final exponentiation on six lanes per check
+void launch_check6_miller(const uint32_t* S, const uint32_t* F, uint32_t n_groups, uint8_t* ok, hipStream_t s,
+                          const uint32_t* sel, uint32_t n_sel, uint32_t* lines, uint8_t* flags);
+// G[sel[q]] = MillerLoop(-g1, S[sel[q]]) on one lane per entry (all n_groups entries when sel is null)
+void launch_group_sig_miller_sel(const uint32_t* S, uint32_t n_groups, const uint32_t* sel, uint32_t n_sel, uint32_t* G,
+                                 hipStream_t s);
 // lane: one lane per group (pairing.hpp miller_loop) instead of a three-wave cooperative workgroup (merged runs)
 void launch_group_sig_miller(const uint32_t* S, uint32_t n_groups, uint32_t* G, hipStream_t s, bool exclusive = false,
                              bool lane = false);

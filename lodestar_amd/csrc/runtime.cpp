@@ -113,7 +113,7 @@ struct Slot {
                                           // Miller lines, the groups' MillerLoop(-g1, S) (parts of stages 5, 7)
   // d_in / h_in: every per-call input packed into one arena (one H2D transfer); d_res / h_res: job errors +
   // group verdicts (one D2H transfer).
-  DevBuf<uint8_t> d_in, d_res, d_bytes, d_ok;
+  DevBuf<uint8_t> d_in, d_res, d_bytes, d_ok, d_fbflags;
   DevBuf<uint32_t> d_work, d_lines, d_S, d_F, d_G, d_list, d_msmB, d_msmW, d_fb;
   DevBuf<uint32_t> d_fkeep;  // the batch pass's per-set Miller values, kept for the fallback (run_shard keep_f)
   HostBuf<uint8_t> h_in, h_res, h_ok;
@@ -129,11 +129,11 @@ struct Slot {
   // the stream buffer growth is ordered on (hipFreeAsync / hipMallocAsync); the slot's previous work is complete
   // whenever it grows a buffer (its dispatcher waits for each run), so only this ordering matters
   void set_stream(hipStream_t st) {
-    for (auto* b : {&d_in, &d_res, &d_bytes, &d_ok}) b->st = st;
+    for (auto* b : {&d_in, &d_res, &d_bytes, &d_ok, &d_fbflags}) b->st = st;
     for (auto* b : {&d_work, &d_lines, &d_S, &d_F, &d_G, &d_list, &d_msmB, &d_msmW, &d_fb, &d_fkeep}) b->st = st;
   }
   void release_all() {
-    d_in.release(); d_res.release(); d_bytes.release(); d_ok.release();
+    d_in.release(); d_res.release(); d_bytes.release(); d_ok.release(); d_fbflags.release();
     d_work.release(); d_lines.release(); d_S.release(); d_F.release(); d_list.release();
     d_msmB.release(); d_msmW.release(); d_fb.release(); d_G.release(); d_fkeep.release();
     h_in.release(); h_res.release(); h_ok.release(); h_list.release();
@@ -221,6 +221,9 @@ struct Options {  // snapshot taken at the start of each call
   int64_t acc6_max = 16384;       // one-item-chunk runs of <= this many chunks take the six-lane accumulation
   int64_t small_max = 4096;       // runs of <= this many sets are latency-first (speculation, cooperative fallback checks)
   int64_t fb_direct_min = 1024;   // large runs under load with >= this many retried jobs check each directly (0 = never)
+  int64_t fb_check6 = 2;          // those runs' lane checks: 0 one lane per check; 1 MillerLoop(-g1, S) one lane and the
+                                  // final exponentiation six lanes per check (gt6.hpp); 2 both on six lanes
+  int64_t fb_force_busy = 0;      // tests: every run's fallback takes the under-load forms
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
            group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&
@@ -230,7 +233,7 @@ struct Options {  // snapshot taken at the start of each call
            lines_lanes == o.lines_lanes && merge_balance == o.merge_balance && coop_max == o.coop_max &&
            coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec &&
            fb_lane_min == o.fb_lane_min && acc6_max == o.acc6_max && small_max == o.small_max &&
-           fb_direct_min == o.fb_direct_min;
+           fb_direct_min == o.fb_direct_min && fb_check6 == o.fb_check6 && fb_force_busy == o.fb_force_busy;
   }
 };
 
@@ -1070,10 +1073,27 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     // group) check every job directly in ONE lane launch: three times the checks of the sub-group round trip, but one
     // ~25 ms lane round instead of two, and the run's call latency is what bounds a loaded device's throughput
     // (calls in flight / latency).  Small runs and runs on an idle device keep the cooperative checks' latency.
-    const bool busy = !small && !sl.alone;
+    const bool busy = (!small && !sl.alone) || opt.fb_force_busy;
     auto lane_checks = [&](uint32_t count) { return busy && opt.fb_lane_min > 0 && count >= (uint32_t)opt.fb_lane_min; };
     const bool direct = (small && nr <= kFbDirectMax) || (busy && opt.fb_direct_min > 0 && nr >= (uint32_t)opt.fb_direct_min);
     const uint32_t nsub = !direct && nr >= 2 * kFbSub ? (nr + kFbSub - 1) / kFbSub : 0;
+    // One check launch of `count` entries (sel null: entries 0 .. ng): cooperative checks (small runs, idle device), or
+    // for many checks under load MillerLoop(-g1, S) one lane per entry and the final exponentiation on six lanes per
+    // check (fb_check6, gt6.hpp), or everything one lane per check
+    auto fb_check = [&](const uint32_t* S, const uint32_t* F, uint32_t ng, uint8_t* ok, const uint32_t* sel,
+                        uint32_t count) {
+      if (lane_checks(count) && opt.fb_check6 == 2) {  // the Miller loop on six lanes too, from stored lines
+        sl.d_lines.ensure((size_t)ng * kMillerLineWords);
+        sl.d_fbflags.ensure(ng);
+        launch_check6_miller(S, F, ng, ok, sfb, sel, count, sl.d_lines.p, sl.d_fbflags.p);
+      } else if (lane_checks(count) && opt.fb_check6) {
+        sl.d_G.ensure((size_t)W_FP12 * ng);
+        launch_group_sig_miller_sel(S, ng, sel, count, sl.d_G.p, sfb);
+        launch_group_check6(F, sl.d_G.p, ng, ok, sfb, sel, count);
+      } else {
+        launch_group_check(S, F, ng, ok, sfb, sel, count, nullptr, false, lane_checks(count));
+      }
+    };
     std::vector<uint32_t> subr(2 * (size_t)nsub);
     for (uint32_t t = 0; t < nsub; t++) {
       subr[2 * t] = t * kFbSub;
@@ -1138,8 +1158,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
         launch_range_combine_lane(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, sfb);
       else
         launch_range_combine(dS, dF, nr, sl.d_list.p + o_sub, nsub, dS_sub, dF_sub, sfb);
-      launch_group_check(dS_sub, dF_sub, nsub, sl.d_ok.p + nr, sfb, nullptr, 0, nullptr, false,
-                         lane_checks(nsub));
+      fb_check(dS_sub, dF_sub, nsub, sl.d_ok.p + nr, nullptr, nsub);
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpyAsync(sl.h_ok.p + nr, sl.d_ok.p + nr, nsub, hipMemcpyDeviceToHost, sfb));
       HIPCHK(hipEventRecord(sl.done, sfb));
@@ -1156,8 +1175,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       const uint32_t ns = (uint32_t)sel.size();
       memcpy(hl + o_sel, sel.data(), (size_t)ns * 4);
       HIPCHK(hipMemcpyAsync(sl.d_list.p + o_sel, hl + o_sel, (size_t)ns * 4, hipMemcpyHostToDevice, sfb));
-      launch_group_check(dS, dF, nr, sl.d_ok.p, sfb, sl.d_list.p + o_sel, ns, nullptr, false,
-                         lane_checks(ns));
+      fb_check(dS, dF, nr, sl.d_ok.p, sl.d_list.p + o_sel, ns);
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpyAsync(sl.h_ok.p, sl.d_ok.p, ns, hipMemcpyDeviceToHost, sfb));
       HIPCHK(hipEventRecord(sl.done, sfb));
@@ -2036,6 +2054,11 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "fb_lane_min") {
     if (value < 0) return BLSGPU_ERR_ARGS;
     ctx->opt.fb_lane_min = value;
+  } else if (k == "fb_force_busy") {
+    ctx->opt.fb_force_busy = value != 0;
+  } else if (k == "fb_check6") {
+    if (value < 0 || value > 2) return BLSGPU_ERR_ARGS;
+    ctx->opt.fb_check6 = value;
   } else if (k == "fb_direct_min") {
     if (value < 0) return BLSGPU_ERR_ARGS;
     ctx->opt.fb_direct_min = value;
@@ -2115,6 +2138,8 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "acc6_max") *value = o.acc6_max;
   else if (k == "small_max") *value = o.small_max;
   else if (k == "fb_direct_min") *value = o.fb_direct_min;
+  else if (k == "fb_check6") *value = o.fb_check6;
+  else if (k == "fb_force_busy") *value = o.fb_force_busy;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }

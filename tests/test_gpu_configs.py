@@ -150,3 +150,27 @@ def test_c5_lane_tails_vs_oracle(ctx):
     finally:
         ctx.set_option("lane_tail_min", 0)
     assert np.array_equal(got, w["expected"])
+
+
+@pytest.mark.parametrize("opts", [
+    {"fb_force_busy": 1, "fb_direct_min": 1, "fb_lane_min": 1},                  # every job: six-lane Miller + gt6
+    {"fb_force_busy": 1, "fb_direct_min": 0, "fb_lane_min": 1, "small_max": 0},  # sub-groups, then jobs
+    {"fb_force_busy": 1, "fb_direct_min": 1, "fb_lane_min": 1, "fb_check6": 1},  # one-lane Miller + gt6
+])
+def test_c5_under_load_fallback_forms_vs_oracle(ctx, opts):
+    """C5's fallback in the forms merged runs take under load (six-lane, or one-lane, MillerLoop(-g1, S) and the six-lane final
+    exponentiation of gt6.hpp per check; per job directly or after sub-groups), forced on a lone call: job for job equal
+    to the oracle, on the reference-shaped workload and on a copy with every corruption class."""
+    w, n, desc, _ = bench.build_workload(ctx, "C5", 0, signer=oracle_sign)
+    table = bench.oracle_table(w)
+    saved = {k: ctx.get_option(k) for k in opts}
+    try:
+        for k, v in opts.items():
+            ctx.set_option(k, v)
+        got, st = compare(ctx, call_of(w), table)
+        assert np.array_equal(got, w["expected"]) and st.fallback_jobs > 0
+        bad, _ = corrupted(w, 0xC6)
+        compare(ctx, bad, table)
+    finally:
+        for k, v in saved.items():
+            ctx.set_option(k, v)

@@ -89,6 +89,12 @@ def test_midsize_one_percent_corrupt_vs_oracle(ctx, pool, n):
     {"fb_lane_min": 1, "coop_max": 0},              # lane-per-check fallback checks (merged runs under load)
     {"coop_max": 0, "acc6_max": 0},                 # two-lane accumulation instead of the six-lane one
     {"coop_max": 0, "miller_lanes": 6, "dedupe": 0},  # six lanes forced
+    # the fallback's under-load forms: one-lane MillerLoop(-g1, S) + six-lane final exponentiations (gt6.hpp), per job
+    # directly or after sub-groups; and the all-one-lane checks
+    {"fb_force_busy": 1, "fb_direct_min": 1, "fb_lane_min": 1},
+    {"fb_force_busy": 1, "fb_direct_min": 0, "fb_lane_min": 1, "small_max": 0},
+    {"fb_force_busy": 1, "fb_direct_min": 1, "fb_lane_min": 1, "fb_check6": 0},
+    {"fb_force_busy": 1, "fb_direct_min": 1, "fb_lane_min": 1, "fb_check6": 1},
 ])
 def test_midsize_forms_agree(ctx, pool, opts):
     saved = {k: ctx.get_option(k) for k in opts}

@@ -1,0 +1,16 @@
+# usage: bash tools/gpurun/r05_p.sh TAG -- check6 parity; C5 under load fb_check6 2 / 1 / 0; trace of check6=2
+set -e
+TAG=$1; shift
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_midsize.py -x -v --timeout 250 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
+i=0
+for V in "" "--set fb_check6=1" "--set fb_check6=0"; do
+  i=$((i+1))
+  echo "$V" > gpurun_out/${TAG}_C5_v$i.args
+  timeout -k 10 200 python -u bench.py --config C5 --inflight 32 --steps 400 --warmup 32 --no-cpu-baseline --no-parity $V > gpurun_out/${TAG}_C5_v$i.json 2> gpurun_out/${TAG}_C5_v$i.err
+done
+R=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_load -o run -- \
+  python3 $R/bench.py --config C5 --inflight 32 --steps 200 --warmup 32 --no-cpu-baseline --no-parity > $R/gpurun_out/${TAG}_load.log 2>&1
