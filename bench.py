@@ -297,6 +297,7 @@ def roofline(runs, n_sets, group_count, pubkeys_per_set, sets_per_s, miller_k=2,
         "unit": "T limb-products/s (32x32->64)",
         "frac": round(achieved * 1e12 / VALU_PEAK_PRODUCTS, 5),
         "traffic": pmc_traffic(KERNEL_OF_STAGE[best], int(round(np.mean([r[1] for r in runs]))) if runs else 0),
+        "traffic_source": pmc_source(),
         "launches_timed": len(runs),
         "sets_per_launch": round(float(np.mean([r[1] for r in runs])), 1) if runs else 0,
         "algorithmic_products_per_launch": round(prod[best] / n_runs),
@@ -314,7 +315,7 @@ def roofline(runs, n_sets, group_count, pubkeys_per_set, sets_per_s, miller_k=2,
     return out
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")
 # grid work-items per distinct message (C2: one message per set) of the hash stage's launches; k_batch_inv runs one
 # lane per INV_K = 16 elements (csrc/k_inv.hip) and twice per stage (before the maps, before the affine conversion),
 # k_hash_map two lanes per message (one SSWU map each)
@@ -338,6 +339,22 @@ def pmc_traffic(kernel, n_sets):
     per_unit = sum((table[p]["FETCH_B_per_item"] + table[p]["WRITE_B_per_item"]) * PMC_ITEMS_PER_UNIT.get(p, 1.0)
                    for p in parts)
     return round(per_unit * n_sets)
+
+
+def pmc_source():
+    """Where `traffic` comes from: the committed PMC file and whether it was measured on the library this process
+    loaded (md5 recorded by tools/pmc_to_json.py) -- a stale file is flagged, never silently reused."""
+    if not os.path.exists(PMC_FILE):
+        return None
+    import hashlib
+
+    from lodestar_amd.native import LIB_PATH
+
+    with open(PMC_FILE) as fh:
+        want = json.load(fh).get("lib_md5")
+    with open(LIB_PATH, "rb") as fh:
+        have = hashlib.md5(fh.read()).hexdigest()
+    return {"file": os.path.relpath(PMC_FILE, ROOT), "measured_on_this_library": want == have}
 
 
 BLST_SETS_PER_CORE = 2200.0  # published anchor: ~0.9 ms/set/thread, x2 batched (BASELINE.md)

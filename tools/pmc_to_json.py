@@ -29,6 +29,18 @@ def per_launch(path, counter):
     return {k: (sum(v) / len(v), len(v), 1024 * sum(v) / max(items[k], 1)) for k, v in acc.items()}
 
 
+def lib_md5(path=None):
+    """md5 of the libblsgpu.so the passes measured (the same file travels to the GPU box): bench.py flags its
+    `traffic` as stale when the library it loads differs."""
+    import hashlib
+    import os
+
+    path = path or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lodestar_amd",
+                                "libblsgpu.so")
+    with open(path, "rb") as fh:
+        return hashlib.md5(fh.read()).hexdigest()
+
+
 def main(prefix, out):
     f = per_launch(f"{prefix}_pmc_FETCH_SIZE/run_counter_collection.csv", "FETCH_SIZE")
     w = per_launch(f"{prefix}_pmc_WRITE_SIZE/run_counter_collection.csv", "WRITE_SIZE")
@@ -43,6 +55,7 @@ def main(prefix, out):
            "units": "kB per launch as reported; gfx950 FETCH_SIZE counts 1/2 of wide streaming reads "
                     "(MI355X_MICROARCH.md HBM section) -> bytes = 2 x 1024 x FETCH_SIZE; WRITE_SIZE exact. "
                     "*_B_per_item: HBM bytes per grid work-item over all dispatches (FETCH already doubled)",
+           "lib_md5": lib_md5(),
            "kernels": kernels}
     with open(out, "w") as fh:
         json.dump(doc, fh, indent=1)
