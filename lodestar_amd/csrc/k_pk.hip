@@ -2,6 +2,9 @@
 // aggregate serialization (PublicKey.aggregate(...).toBytes()), KeyValidate and the table upload decoder.
 #include "k_common.hpp"
 
+#ifndef BLSGPU_PK_AGG_GROUPS
+#define BLSGPU_PK_AGG_GROUPS 1
+#endif
 // One wave per set: strided partial sums of the set's pubkeys, then an LDS tree reduction.  Table mode reads
 // pk_table[pk_index[k]]; bytes-aggregate mode decodes pk_bytes[96 k] (trusted keys, PublicKey.fromBytes
 // without subgroup check, as the pool worker, worker.ts:110-116: an identity key adds nothing).  The first
@@ -91,6 +94,77 @@ __global__ __launch_bounds__(WAVE) void k_pk_aggregate(PipelineBuffers b, uint32
     __syncthreads();
   }
   if (lane == 0) st_g1j(b.pk_jac, b.n, set, acc);
+}
+
+// The same aggregation on L lanes per set (64 / L sets per wave; L = 8, 16 or 32), the partial sums reduced by an
+// in-register butterfly (__shfl_xor inside the lane group, no LDS, no barrier): with many sets (C4: 32,768 sets of
+// ~486 keys) a wave per set spent ~2x the useful additions in its 6-level tree and idle lanes; L is chosen so the
+// launch still gives every SIMD a wave (launch_pk_aggregate).
+BLS_INL fp fp_shfl_xor(const fp& x, int m) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < BLS_NL; i++) r.l[i] = (uint32_t)__shfl_xor((int)x.l[i], m);
+  return r;
+}
+template <int L>
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_pk_aggregate_g(PipelineBuffers b, uint32_t n_sets) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x, t = q % L;
+  const uint32_t si = q / L;
+  const bool on = si < n_sets;  // whole groups: n_sets * L lanes, groups never straddle a wave (L divides WAVE)
+  const uint32_t set = on ? (b.agg_sets ? b.agg_sets[si] : si) : 0;
+  const uint32_t first = on ? b.set_pk_first[set] : 0, last = on ? b.set_pk_first[set + 1] : 0;
+  g1j acc = jac_infinity<fp>();
+  uint32_t my_err_k = 0xffffffffu;
+  int my_err = 0;
+  for (uint32_t k = first + t; k < last; k += L) {
+    g1a pt;
+    if (b.pk_bytes) {
+      uint8_t raw[96];
+      const uint8_t* src = b.pk_bytes + (size_t)k * 96;
+#pragma unroll
+      for (int z = 0; z < 96; z++) raw[z] = src[z];
+      bool inf = false;
+      const int st = pk_decode96(raw, pt, inf);
+      if (st != BLS_OK) {
+        if (my_err == 0) {
+          my_err = st;
+          my_err_k = k;
+        }
+        continue;
+      }
+      if (inf) continue;
+    } else {
+      const uint32_t idx = b.pk_index[k];
+      if (idx >= b.pk_table_n) {
+        if (my_err == 0) {
+          my_err = BLS_DEVICE_ERROR;
+          my_err_k = k;
+        }
+        continue;
+      }
+      pt = ld_pktab(b.pk_table, idx);
+    }
+    acc = jac_add_aff(acc, pt);
+  }
+  // butterfly: after log2 L levels every lane of the group holds the sum (and the first error by key position)
+#pragma unroll 1
+  for (int m = L / 2; m >= 1; m >>= 1) {
+    g1j o;
+    o.x = fp_shfl_xor(acc.x, m);
+    o.y = fp_shfl_xor(acc.y, m);
+    o.z = fp_shfl_xor(acc.z, m);
+    const uint32_t ok = (uint32_t)__shfl_xor((int)my_err_k, m);
+    const int oc = __shfl_xor(my_err, m);
+    if (ok < my_err_k) {
+      my_err_k = ok;
+      my_err = oc;
+    }
+    acc = jac_add(acc, o);
+  }
+  if (on && t == 0) {
+    b.status[2 * b.n + set] = (int8_t)my_err;
+    st_g1j(b.pk_jac, b.n, set, acc);
+  }
 }
 
 // The set's (aggregated) public key as a Jacobian point + status.  Single-key bytes mode decodes pk_bytes;
@@ -241,9 +315,20 @@ __global__ __launch_bounds__(WAVE) void k_pk_table_fill(const uint8_t* pk96, uin
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
+// lanes per set: one wave per set while n sets leave SIMDs idle, else the fewest lanes (>= 8) that still give
+// every SIMD a wave (n * L >= 65,536 lanes)
 void launch_pk_aggregate(const PipelineBuffers& b, uint32_t n, hipStream_t s) {
   if (b.agg_sets) n = b.n_agg;
-  if (n) hipLaunchKernelGGL(k_pk_aggregate, dim3(n), dim3(WAVE), 0, s, b, n);
+  if (!n) return;
+  const uint32_t lanes = 1024 * WAVE;
+  if ((uint64_t)n * 64 <= lanes || !BLSGPU_PK_AGG_GROUPS)
+    hipLaunchKernelGGL(k_pk_aggregate, dim3(n), dim3(WAVE), 0, s, b, n);
+  else if ((uint64_t)n * 32 <= 2 * lanes)
+    hipLaunchKernelGGL(k_pk_aggregate_g<32>, dim3((n * 32 + WAVE - 1) / WAVE), dim3(WAVE), 0, s, b, n);
+  else if ((uint64_t)n * 16 <= 2 * lanes)
+    hipLaunchKernelGGL(k_pk_aggregate_g<16>, dim3((n * 16 + WAVE - 1) / WAVE), dim3(WAVE), 0, s, b, n);
+  else
+    hipLaunchKernelGGL(k_pk_aggregate_g<8>, dim3((n * 8 + WAVE - 1) / WAVE), dim3(WAVE), 0, s, b, n);
 }
 void launch_pk_finish(const PipelineBuffers& b, uint32_t n, hipStream_t s) {
   // pk status lives right after the set status array (runtime allocates 3 * stride bytes)

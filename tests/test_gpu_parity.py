@@ -239,6 +239,29 @@ def test_aggregate_pubkeys_golden_and_oracle(ctx):
     assert gst[9] == 9 and gst[10] == bls.BLST_BAD_ENCODING  # EMPTY_AGGREGATE_ARRAY, malformed key
 
 
+@pytest.mark.parametrize("n_sets", [2000, 5000, 9000])
+def test_aggregate_pubkeys_lane_groups_vs_oracle(ctx, n_sets):
+    """The aggregation's lane-group forms (k_pk_aggregate_g: 32 / 16 / 8 lanes per set, chosen by the number of sets,
+    in-register butterfly) on many small aggregates in bytes-aggregate mode, with malformed keys at several positions
+    and empty sets: statuses and both encodings byte-identical to the oracle."""
+    rng = np.random.default_rng(n_sets)
+    pool = cpu.sk_to_pk(interop_sks(512), threads=THREADS)
+    sizes = rng.integers(0, 12, n_sets)
+    spf = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    sel = rng.integers(0, 512, int(spf[-1]))
+    kb = bytearray(b"".join(pool[96 * i: 96 * i + 96] for i in sel))
+    for s in rng.choice(n_sets, 20, replace=False):
+        if sizes[s] >= 2:
+            kb[96 * (spf[s] + int(rng.integers(0, sizes[s])))] |= 0x80  # compressed flag on a 96-byte key
+    for out_len in (96, 48):
+        got, gst = ctx.aggregate_pubkeys(pk_bytes=bytes(kb), set_pk_first=spf, out_len=out_len)
+        want, wst = cpu.aggregate_pubkeys(out_len=out_len, job_first_set=[0, n_sets], sigs=bytes(96 * n_sets),
+                                          sig_len=[96] * n_sets, msgs=bytes(32 * n_sets), pk_bytes=bytes(kb),
+                                          set_pk_first=spf, threads=THREADS)
+        assert list(gst) == list(wst) and got == want
+    assert (gst == bls.BLST_BAD_ENCODING).sum() >= 5 and (gst == 9).sum() >= 1
+
+
 def test_bytes_aggregate_mode_golden(ctx):
     """Aggregate ISignatureSets from per-key bytes (any PublicKey objects, attestation.ts:131-138) on every
     golden case."""
