@@ -15,7 +15,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.environ.get("BLSGPU_LIB") or os.path.join(PKG, "libblsgpu.so")  # override: tuning variants
 ARCH = os.environ.get("BLSGPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["k_sig.hip", "k_msm.hip", "k_hash.hip", "k_pk.hip", "k_miller.hip", "k_group.hip", "k_inv.hip", "k_ssz.hip", "k_debug.hip",
+SOURCES = ["k_sig.hip", "k_msm.hip", "k_hash.hip", "k_hmap.hip", "k_pk.hip", "k_miller.hip", "k_group.hip", "k_inv.hip", "k_ssz.hip", "k_debug.hip",
            "runtime.cpp"]
 
 
@@ -45,7 +45,7 @@ def tu_defines():
 # wave per SIMD, so occupancy-driven scheduling buys nothing there (C2 +1.5% at 20 steps, +1.7% at 100; the same
 # strategy on every TU lost 6%: the Miller accumulation and the decode spill more under it).
 _ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-TU_CFLAGS = {"k_hash.hip": _ILP, "k_pk.hip": _ILP}
+TU_CFLAGS = {"k_hash.hip": _ILP, "k_hmap.hip": _ILP, "k_pk.hip": _ILP}
 
 
 def tu_cflags():

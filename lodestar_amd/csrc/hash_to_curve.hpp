@@ -258,18 +258,23 @@ BLS_HDNI g2j clear_cofactor_g2(const g2j& P) {
 // instead of registers, reordered so that only the accumulator is live across each [|z|] chain:
 //   A = [|z|]P,   C = psi^2(2P) - psi(P) + A - P,   D = [|z|](A - psi(P)),   h_eff P = C + D
 // (clear_cofactor_g2's t3 + t2 - t1 - P with t1 = -A, t2 = D, t3 = psi^2(2P) - psi(P)).  Slot 0 holds P on entry;
-// slots 1 and 2 are overwritten.  Slot 1 may be slot 0 itself (P is in registers before slot 1 is written).
-template <class Ld, class St>
-BLS_INL g2j clear_cofactor_g2_slots(Ld ld, St st) {
-  const g2j A = jac_mul_zabs_ld<fp2>([&] { return ld(0); });
+// slots 1 and 2 are overwritten.  Slot 1 may be slot 0 itself (P is in registers before slot 1 is written).  Over
+// any G2 field type F (fp2, or the lane-pair fp2x of fp2x.hpp).
+template <class F, class Ld, class St>
+BLS_INL jac<F> clear_cofactor_slots(Ld ld, St st) {
+  const jac<F> A = jac_mul_zabs_ld<F>([&] { return ld(0); });
   {
-    const g2j P = ld(0);
-    const g2j psiP = g2_psi(P);
+    const jac<F> P = ld(0);
+    const jac<F> psiP = g2_psi(P);
     st(1, jac_add(A, jac_neg(psiP)));
     st(2, jac_add(jac_add(g2_psi2(jac_dbl(P)), jac_neg(psiP)), jac_add(A, jac_neg(P))));
   }
-  const g2j D = jac_mul_zabs_ld<fp2>([&] { return ld(1); });
+  const jac<F> D = jac_mul_zabs_ld<F>([&] { return ld(1); });
   return jac_add(D, ld(2));
+}
+template <class Ld, class St>
+BLS_INL g2j clear_cofactor_g2_slots(Ld ld, St st) {
+  return clear_cofactor_slots<fp2>(ld, st);
 }
 
 // hash_to_G2 in two halves around the one inversion of the two maps, so a kernel can batch that inversion over

@@ -45,7 +45,7 @@ static_assert(2 * WAVE <= BLS_FP2_LDS_LANES, "128-lane kernels (gt_wave.hpp, k_m
 #define BLSGPU_WPE_HASH BLSGPU_WPE
 #endif
 #ifndef BLSGPU_WPE_HMAP
-#define BLSGPU_WPE_HMAP BLSGPU_WPE_HASH
+#define BLSGPU_WPE_HMAP 2
 #endif
 #ifndef BLSGPU_WPE_GRP
 #define BLSGPU_WPE_GRP BLSGPU_WPE

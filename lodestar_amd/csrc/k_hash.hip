@@ -6,8 +6,12 @@
 // k_hash_clear (sum, cofactor clearing; Jacobian H(m) + N(z)) -> k_batch_inv(N(z)) -> k_h_affine.
 #include "k_common.hpp"
 #include "g2_coop.hpp"
+#include "fp2x.hpp"
 
 #define W_HPREP (7 * 2 * W_FP)
+#ifndef BLSGPU_HASH_PAIRS
+#define BLSGPU_HASH_PAIRS 1
+#endif
 
 __device__ __forceinline__ void st_prep(uint32_t* p, uint32_t n, uint32_t u, const h2c_prep& h) {
   st_fp2(p, n, u, 0 * W_FP, h.u0);
@@ -18,18 +22,6 @@ __device__ __forceinline__ void st_prep(uint32_t* p, uint32_t n, uint32_t u, con
   st_fp2(p, n, u, 10 * W_FP, h.tv1);
   st_fp2(p, n, u, 12 * W_FP, h.d);
 }
-__device__ __forceinline__ h2c_prep ld_prep(const uint32_t* p, uint32_t n, uint32_t u) {
-  h2c_prep h;
-  h.u0 = ld_fp2(p, n, u, 0 * W_FP);
-  h.u1 = ld_fp2(p, n, u, 2 * W_FP);
-  h.Zu2_0 = ld_fp2(p, n, u, 4 * W_FP);
-  h.Zu2_1 = ld_fp2(p, n, u, 6 * W_FP);
-  h.tv0 = ld_fp2(p, n, u, 8 * W_FP);
-  h.tv1 = ld_fp2(p, n, u, 10 * W_FP);
-  h.d = ld_fp2(p, n, u, 12 * W_FP);
-  return h;
-}
-
 STAGE_KERNEL void k_hash_prep(PipelineBuffers b) {
   uint32_t u = blockIdx.x * WAVE + threadIdx.x;
   if (u >= b.n_umsg) return;
@@ -43,19 +35,6 @@ STAGE_KERNEL void k_hash_prep(PipelineBuffers b) {
   hash_to_g2_prep(msg, h);
   st_prep(b.h_prep, b.nm, u, h);
   st_fp(b.h_norm, b.nm, u, 0, fp2_norm(h.d));
-}
-
-// inv: 1 / N(d) from the batch inversion; d^-1 = conj(d) / N(d).  Two lanes per message (lane pair (u, j)): each
-// runs one SSWU map + isogeny -> h_q[j] (the two maps of a message are independent, so a small call's hash
-// latency drops by one map).
-STAGE_KERNEL_W(BLSGPU_WPE_HMAP) void k_hash_map(PipelineBuffers b, const uint32_t* inv) {
-  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
-  if (q >= 2 * b.n_umsg) return;
-  const uint32_t u = q >> 1, j = q & 1;
-  const h2c_prep h = ld_prep(b.h_prep, b.nm, u);
-  const fp ni = ld_fp(inv, b.n_umsg, u, 0);
-  const fp2 dinv = fp2_make(fp_mul(h.d.c0, ni), fp_neg(fp_mul(h.d.c1, ni)));
-  st_g2j(b.h_q, 2 * b.nm, q, hash_to_g2_map_j(h, dinv, (int)j));
 }
 
 // Q = q0 + q1, cofactor clearing (RFC 9380 G.3); Jacobian out + N(z) for the batched affine conversion.  The
@@ -78,6 +57,56 @@ STAGE_KERNEL_W(BLSGPU_WPE_HASH) void k_hash_clear(PipelineBuffers b) {
       });
   st_g2j(b.h_jac, b.nm, u, H);
   st_fp(b.h_norm, b.nm, u, 0, fp2_norm(H.z));
+}
+
+// The same clearing on lane pairs (fp2x.hpp): lane 2m + k holds coefficient k of every Fp2 coordinate of message m's
+// points, so a lane carries half a point and the kernel runs two waves per SIMD without spills.  The chain bases live
+// in this lane's LDS slot (its coefficients only), C in h_jac[m] (coefficient k in the words of c_k).
+#ifndef BLSGPU_WPE_HASH2
+#define BLSGPU_WPE_HASH2 2
+#endif
+__device__ __forceinline__ g2jx ld_g2jx(const uint32_t* p, uint32_t n, uint32_t i, uint32_t k) {
+  g2jx r;
+  r.x.v = ld_fp(p, n, i, (int)(k * W_FP));
+  r.y.v = ld_fp(p, n, i, (int)((2 + k) * W_FP));
+  r.z.v = ld_fp(p, n, i, (int)((4 + k) * W_FP));
+  return r;
+}
+__device__ __forceinline__ void st_g2jx(uint32_t* p, uint32_t n, uint32_t i, uint32_t k, const g2jx& v) {
+  st_fp(p, n, i, (int)(k * W_FP), v.x.v);
+  st_fp(p, n, i, (int)((2 + k) * W_FP), v.y.v);
+  st_fp(p, n, i, (int)((4 + k) * W_FP), v.z.v);
+}
+// this lane's slot: coordinate c at words c * W_FP .. + 13
+__device__ __forceinline__ g2jx ld_g2jx_slot(const uint32_t* s, uint32_t t) {
+  g2jx r;
+  r.x.v = ld_fp(s, WAVE, t, 0);
+  r.y.v = ld_fp(s, WAVE, t, W_FP);
+  r.z.v = ld_fp(s, WAVE, t, 2 * W_FP);
+  return r;
+}
+__device__ __forceinline__ void st_g2jx_slot(uint32_t* s, uint32_t t, const g2jx& v) {
+  st_fp(s, WAVE, t, 0, v.x.v);
+  st_fp(s, WAVE, t, W_FP, v.y.v);
+  st_fp(s, WAVE, t, 2 * W_FP, v.z.v);
+}
+STAGE_KERNEL_W(BLSGPU_WPE_HASH2) void k_hash_clear2(PipelineBuffers b) {
+  __shared__ uint32_t base[3 * W_FP * WAVE];
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x, u = q >> 1, k = q & 1;
+  if (u >= b.n_umsg) return;  // per pair: both lanes of a message leave together
+  const uint32_t qs = 2 * b.nm, t = threadIdx.x;
+  st_g2jx_slot(base, t, jac_add(ld_g2jx(b.h_q, qs, 2 * u, k), ld_g2jx(b.h_q, qs, 2 * u + 1, k)));
+  const g2jx H = clear_cofactor_slots<fp2x>(
+      [&](int s) { return s == 2 ? ld_g2jx(b.h_jac, b.nm, u, k) : ld_g2jx_slot(base, opaque_u32(t)); },
+      [&](int s, const g2jx& v) {
+        if (s == 2)
+          st_g2jx(b.h_jac, b.nm, u, k, v);
+        else
+          st_g2jx_slot(base, t, v);
+      });
+  st_g2jx(b.h_jac, b.nm, u, k, H);
+  const fp nz = fp2x_norm(H.z);
+  if (k == 0) st_fp(b.h_norm, b.nm, u, 0, nz);
 }
 
 // The same clearing for small runs, latency first: one 16-lane group per message (g2_coop.hpp), four per workgroup;
@@ -151,10 +180,12 @@ void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s, bool coop, bool 
   if (!b.n_umsg) return;
   hipLaunchKernelGGL(k_hash_prep, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
   launch_batch_inv(b.h_norm, b.nm, 0, b.inv_buf, b.n_umsg, s);
-  hipLaunchKernelGGL(k_hash_map, grid_for(2 * b.n_umsg), dim3(WAVE), 0, s, b, b.inv_buf);
+  launch_hash_map(b, b.inv_buf, s);
   if (coop)
     hipLaunchKernelGGL(k_hash_clear_coop, dim3((b.n_umsg + HC_GROUPS - 1) / HC_GROUPS), dim3(WAVE),
                        BLSGPU_EXCLUSIVE_SMALL && exclusive ? exclusive_cu_lds<k_hash_clear_coop>() : 0, s, b);
+  else if (BLSGPU_HASH_PAIRS)
+    hipLaunchKernelGGL(k_hash_clear2, grid_for(2 * b.n_umsg), dim3(WAVE), 0, s, b);
   else
     hipLaunchKernelGGL(k_hash_clear, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
 }

@@ -10,11 +10,12 @@
 //                   prod_i e(r_i pk_i, H(m)) = e(sum_i r_i pk_i, H(m))).
 //   k_miller_acc2:  the same accumulation on TWO lanes per chunk, each holding half of f (no spills): the default
 //                   for one-item chunks (runs below 131,072 pairings); chunks of >= 2 stay on one lane (faster).
-//   k_miller_lines2 (two lanes per message) and k_miller_coop (one 192-lane workgroup per pairing, small runs).
+//   k_miller_lines2 (lane pairs, fp2x.hpp) and k_miller_coop (one 192-lane workgroup per pairing, small runs).
 // Line traffic is 68 x 84 words = 22.8 KB per message (HBM-cheap next to ~5,200 Montgomery products).
 #include "k_common.hpp"
 #include "gt_wave.hpp"
 #include "gt6.hpp"
+#include "fp2x.hpp"
 
 // Line pairs in the one-lane chunk loop (line_pair + fp12_mul_by_line2: 23 Fp2 products per two items instead of 26):
 // correct (test_line_pair_product, chunk-form GPU parity) but the pending line and the denser product raise the
@@ -38,61 +39,46 @@ STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_miller_lines(PipelineBuffers b) {
   miller_lines_store(ld_g2a(b.h_aff, b.nm, u), b.lines, b.nm, u);
 }
 
-// The same lines on TWO lanes per message (mid-size runs, latency): both lanes hold T; a doubling step's products run
-// as two phases of independent products split over the pair (phase 1: lane 0 X Y, Y^2, X^2 | lane 1 Z^2, (Y + Z)^2;
-// phase 2: lane 0 A (B - F), B H | lane 1 E^2, G^2), the partner's results arriving by lane exchanges: 5 product
-// times per doubling instead of 9.  The five addition steps run on both lanes.  Lane h stores word half h of the line.
-STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_miller_lines2(PipelineBuffers b) {
+// The same lines on lane pairs (fp2x.hpp): lane 2u + k holds coefficient k of T's coordinates and stores coefficient
+// k of each line element -- half the per-lane state, two waves per SIMD.  Q is re-read at the five addition steps.
+#ifndef BLSGPU_WPE_LINES2
+#define BLSGPU_WPE_LINES2 2
+#endif
+STAGE_KERNEL_W(BLSGPU_WPE_LINES2) void k_miller_lines2(PipelineBuffers b) {
   const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
-  const uint32_t u = q >> 1, h = q & 1;
+  const uint32_t u = q >> 1, k = q & 1;
   if (u >= b.n_umsg || (b.mflags[u] & MF_H_INF)) return;  // both lanes of a pair leave together
-  const g2a Q = ld_g2a(b.h_aff, b.nm, u);
-  g2proj Tp;
-  Tp.x = Q.x;
-  Tp.y = Q.y;
-  Tp.z = fp2_one();
+  auto ldQ = [&] {
+    const uint32_t uu = opaque_u32(u);
+    aff<fp2x> Q;
+    Q.x.v = ld_fp(b.h_aff, b.nm, uu, (int)(k * W_FP));
+    Q.y.v = ld_fp(b.h_aff, b.nm, uu, (int)((2 + k) * W_FP));
+    return Q;
+  };
+  g2projx Tp;
+  {
+    const aff<fp2x> Q = ldQ();
+    Tp.x = Q.x;
+    Tp.y = Q.y;
+    Tp.z = F_one((const fp2x*)0);
+  }
   int bit = 62;
   bool add_next = false;
 #pragma unroll 1
   for (int s = 0; s < MILLER_STEPS; s++) {
-    line3 Ln;
+    line3x Ln;
     if (!add_next) {
-      // phase 1
-      const fp2 p0 = fp2_mul(h ? Tp.z : Tp.x, h ? Tp.z : Tp.y);          // lane 0: X Y      lane 1: Z^2
-      const fp2 p1 = fp2_sqr(h ? fp2_add_norm(Tp.y, Tp.z) : Tp.y);      // lane 0: Y^2      lane 1: (Y + Z)^2
-      const fp2 p2 = fp2_sqr(Tp.x);                                    // lane 0: X^2      (lane 1: unused)
-      const fp2 o0 = fp2_xlane(p0), o1 = fp2_xlane(p1), o2 = fp2_xlane(p2);
-      const fp2 XY = h ? o0 : p0, C = h ? p0 : o0, B = h ? o1 : p1, S = h ? p1 : o1, J = h ? o2 : p2;
-      const fp2 A = fp2_half(XY);
-      const fp2 xC = fp2_make(fp_lc(T<1>(C.c0), T<-1>(C.c1)), fp_lc(T<1>(C.c0), T<1>(C.c1)));
-      const fp2 E = F_lc(L<12>(xC));
-      const fp2 G = fp2_half(F_lc(L<1>(B), L<3>(E)));
-      const fp2 H = F_lc(L<1>(S), L<-1>(B), L<-1>(C));
-      // phase 2
-      const fp2 q0 = fp2_mul(h ? E : A, h ? E : F_lc(L<1>(B), L<-3>(E)));  // lane 0: A (B - F)   lane 1: E^2
-      const fp2 q1 = fp2_mul(h ? G : B, h ? G : H);                       // lane 0: B H         lane 1: G^2
-      const fp2 r0 = fp2_xlane(q0), r1 = fp2_xlane(q1);
-      const fp2 E2 = h ? q0 : r0, G2 = h ? q1 : r1;
-      Tp.x = h ? r0 : q0;
-      Tp.z = h ? r1 : q1;
-      Tp.y = F_lc(L<1>(G2), L<-3>(E2));
-      Ln.l0 = F_lc(L<1>(E), L<-1>(B));
-      Ln.c1 = F_lc(L<3>(J));
-      Ln.c4 = F_lc(L<-1>(H));
+      miller_dbl_line(Tp, Ln);
       add_next = (BLS_Z_ABS >> bit) & 1ull;
       bit--;
     } else {
-      miller_add_line(Tp, Q, Ln);
+      miller_add_line(Tp, ldQ(), Ln);
       add_next = false;
     }
     uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
-    if (h) {
-      st_fp(o, b.nm, u, 3 * W_FP, Ln.c1.c1);
-      st_fp2(o, b.nm, u, 4 * W_FP, Ln.c4);
-    } else {
-      st_fp2(o, b.nm, u, 0, Ln.l0);
-      st_fp(o, b.nm, u, 2 * W_FP, Ln.c1.c0);
-    }
+    st_fp(o, b.nm, u, (int)(k * W_FP), Ln.l0.v);
+    st_fp(o, b.nm, u, (int)((2 + k) * W_FP), Ln.c1.v);
+    st_fp(o, b.nm, u, (int)((4 + k) * W_FP), Ln.c4.v);
   }
 }
 

@@ -2,9 +2,23 @@
 // of the random linear combination (A9), one lane per signature set.
 #include "k_common.hpp"
 #include "g2_coop.hpp"
+#include "fp2x.hpp"
 
-// check_group == false: the subgroup check is left to k_sig_subgroup_coop (small runs)
-STAGE_KERNEL_W(BLSGPU_WPE_DEC) void k_sig_decode(PipelineBuffers b, uint32_t n_sets, bool check_group) {
+// check_group == false: the subgroup check is left to k_sig_subgroup_coop (small runs) or k_sig_subgroup2 (lane
+// pairs, BLSGPU_SIG_PAIRS); the decode alone then fits two waves per SIMD (WPE_DEC0)
+#ifndef BLSGPU_SIG_PAIRS
+#define BLSGPU_SIG_PAIRS 1
+#endif
+#ifndef BLSGPU_WPE_DEC0
+#define BLSGPU_WPE_DEC0 2
+#endif
+#ifndef BLSGPU_WPE_SUB2
+#define BLSGPU_WPE_SUB2 2
+#endif
+template <bool CHECK, int WPE>
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_sig_decode(
+    PipelineBuffers b, uint32_t n_sets) {
+  const bool check_group = CHECK;
   uint32_t i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= n_sets) return;
   uint8_t raw[192];
@@ -30,6 +44,28 @@ STAGE_KERNEL_W(BLSGPU_WPE_DEC) void k_sig_decode(PipelineBuffers b, uint32_t n_s
   }
   b.flags[i] = inf ? SF_SIG_INF : 0;  // sig flags: flags[0, n)
   b.status[i] = (int8_t)st;
+}
+
+// The subgroup check psi(P) == [z]P of the decoded signatures on lane pairs (fp2x.hpp): lane 2i + k holds coefficient
+// k of every Fp2 coordinate of signature i's chain -- half a point per lane, two waves per SIMD.  The affine P is
+// re-read from the decode's output at each of the chain's mixed additions (curve.hpp jac_mul_zabs_lda).  A failing
+// signature becomes POINT_NOT_IN_GROUP with a zero point, as in k_sig_decode.
+STAGE_KERNEL_W(BLSGPU_WPE_SUB2) void k_sig_subgroup2(PipelineBuffers b, uint32_t n_sets) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x, i = q >> 1, k = q & 1;
+  if (i >= n_sets || b.status[i] != BLS_OK || (b.flags[i] & SF_SIG_INF)) return;  // per pair
+  auto ldP = [&] {
+    const uint32_t ii = opaque_u32(i);
+    aff<fp2x> a;
+    a.x.v = ld_fp(b.sig_aff, b.n, ii, (int)(k * W_FP));
+    a.y.v = ld_fp(b.sig_aff, b.n, ii, (int)((2 + k) * W_FP));
+    return a;
+  };
+  const g2jx zP = jac_neg(jac_mul_zabs_lda<fp2x>(ldP));
+  if (!jac_eq(g2_psi(jac_from_aff(ldP())), zP)) {
+    st_fp(b.sig_aff, b.n, i, (int)(k * W_FP), fp_zero());
+    st_fp(b.sig_aff, b.n, i, (int)((2 + k) * W_FP), fp_zero());
+    if (k == 0) b.status[i] = (int8_t)BLS_POINT_NOT_IN_GROUP;
+  }
 }
 
 // r_i sig_i with the batch scalar word (0 = r = 1, CoreVerify); the signed-window table goes to b.scal_tab.
@@ -87,9 +123,14 @@ void launch_spec_mask(const PipelineBuffers& b, uint32_t n, uint8_t* spec, hipSt
 void launch_sig_decode(const PipelineBuffers& b, uint32_t n, hipStream_t s, bool coop, hipEvent_t decoded,
                        bool exclusive) {
   if (!n) return;
-  hipLaunchKernelGGL(k_sig_decode, grid_for(n), dim3(WAVE), 0, s, b, n, !coop);
+  if (coop || BLSGPU_SIG_PAIRS)
+    hipLaunchKernelGGL((k_sig_decode<false, BLSGPU_WPE_DEC0>), grid_for(n), dim3(WAVE), 0, s, b, n);
+  else
+    hipLaunchKernelGGL((k_sig_decode<true, BLSGPU_WPE_DEC>), grid_for(n), dim3(WAVE), 0, s, b, n);
   if (decoded) (void)hipEventRecord(decoded, s);
-  if (coop)
+  if (!coop) {
+    if (BLSGPU_SIG_PAIRS) hipLaunchKernelGGL(k_sig_subgroup2, grid_for(2 * n), dim3(WAVE), 0, s, b, n);
+  } else
     hipLaunchKernelGGL(k_sig_subgroup_coop, dim3((n + SG_GROUPS - 1) / SG_GROUPS), dim3(WAVE),
                        BLSGPU_EXCLUSIVE_SMALL && exclusive ? exclusive_cu_lds<k_sig_subgroup_coop>() : 0, s, b, n);
 }
