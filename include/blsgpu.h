@@ -162,8 +162,9 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * flight, a slot forming a run waits up to this long for more calls to merge, default 2000; an idle device starts
  * at once), "idle_wait_us" (an idle device lingers up to this long while calls keep arriving, default 0), "merge_balance"
  * (a backlog above merge_sets is cut into equal runs, 0/1, default 0), "miller_lanes" (lanes per Miller accumulation chunk: 0 = auto, the default -- two lanes
- * for one-item chunks (each holding half of f), one lane for shared-squaring chunks; 1 = one lane; 2 = two lanes),
- * "lines_lanes" (lanes per message of the Miller lines, 1 (default) or 2), "msm_slice_mid" (MSM slice length of runs
+ * for one-item chunks (each holding half of f), one lane for shared-squaring chunks; 1 = one lane; 2 = two lanes; 3 =
+ * lane pairs; 6 = six lanes),
+ * "lines_lanes" (lanes per message of the Miller lines: 1, or 2 = lane pairs (default)), "msm_slice_mid" (MSM slice length of runs
  * of 1k-32k sets, 8..256, default 32), "msm_tree" (those runs sum each range's slices by a pairwise tree, 0/1,
  * default 1), "f_run_max" (merged runs: longest lane-serial run of the F product tree, a power of two, default 16),
  * "coop_max" / "coop_g2_max" (runs of <= this many pairings / sets take the cooperative Miller loops / [|z|] chains,
@@ -171,7 +172,9 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * 512), "rsig_spec" (small idle runs form every r_i sig_i beside the batch pass for a possible fallback, 0/1, default
  * 1), "fb_lane_min" (fallback check launches of >= this many checks in large runs take one lane per check, default
  * 256, 0 = never), "route_split_sets" (see blsgpu_route_call, default 16384), "acc6_max" (runs of one-item Miller chunks up to this many
- * take the six-lane accumulation, default 16384; "miller_lanes" 6 forces it),
+ * take the six-lane accumulation, default 16384; "miller_lanes" 6 forces it), "miller_pairs" (larger runs take the
+ * lane-pair accumulation, every Fp2 split over two lanes at two waves per SIMD, 0/1, default 0; "miller_lanes" 3
+ * forces it for every run),
  * "lane_tail_min" / "lane_tail_parts" (runs of >= lane_tail_min sets take lane forms of the Horner passes (bit 0)
  * and of MillerLoop(-g1, S) (bit 1) instead of the cooperative workgroups; default 0 = never, parts 3), "serial"
  * (diagnostics: every branch of a run on one stream, so each kernel runs alone on the chip; 0/1, default 0), "profile" (per-stage kernel times in

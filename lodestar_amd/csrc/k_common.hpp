@@ -6,6 +6,7 @@
 
 #include "kernels.h"
 #include "ops.hpp"
+#include "fp2x.hpp"
 
 #define WAVE 64
 #if defined(__HIP_DEVICE_COMPILE__) && !BLS_INLINE_PRODUCTS && !BLS_FP2_CLASSIC
@@ -137,6 +138,19 @@ __device__ __forceinline__ void st_fp12(uint32_t* p, uint32_t n, uint32_t i, con
   st_fp2(p, n, i, 6 * W_FP, f.c1.c0);
   st_fp2(p, n, i, 8 * W_FP, f.c1.c1);
   st_fp2(p, n, i, 10 * W_FP, f.c1.c2);
+}
+// lane pairs (fp2x.hpp): coefficient k of every Fp2 coordinate of SoA point i (c_k at words (2 c + k) W_FP ..)
+__device__ __forceinline__ g2jx ld_g2jx(const uint32_t* p, uint32_t n, uint32_t i, uint32_t k) {
+  g2jx r;
+  r.x.v = ld_fp(p, n, i, (int)(k * W_FP));
+  r.y.v = ld_fp(p, n, i, (int)((2 + k) * W_FP));
+  r.z.v = ld_fp(p, n, i, (int)((4 + k) * W_FP));
+  return r;
+}
+__device__ __forceinline__ void st_g2jx(uint32_t* p, uint32_t n, uint32_t i, uint32_t k, const g2jx& v) {
+  st_fp(p, n, i, (int)(k * W_FP), v.x.v);
+  st_fp(p, n, i, (int)((2 + k) * W_FP), v.y.v);
+  st_fp(p, n, i, (int)((4 + k) * W_FP), v.z.v);
 }
 // lane-pair exchange (lane ^ 1) of register values: __shfl_xor, no LDS
 BLS_INL fp fp_xlane(const fp& x) {

@@ -6,7 +6,6 @@
 // k_hash_clear (sum, cofactor clearing; Jacobian H(m) + N(z)) -> k_batch_inv(N(z)) -> k_h_affine.
 #include "k_common.hpp"
 #include "g2_coop.hpp"
-#include "fp2x.hpp"
 
 #define W_HPREP (7 * 2 * W_FP)
 #ifndef BLSGPU_HASH_PAIRS
@@ -65,18 +64,6 @@ STAGE_KERNEL_W(BLSGPU_WPE_HASH) void k_hash_clear(PipelineBuffers b) {
 #ifndef BLSGPU_WPE_HASH2
 #define BLSGPU_WPE_HASH2 2
 #endif
-__device__ __forceinline__ g2jx ld_g2jx(const uint32_t* p, uint32_t n, uint32_t i, uint32_t k) {
-  g2jx r;
-  r.x.v = ld_fp(p, n, i, (int)(k * W_FP));
-  r.y.v = ld_fp(p, n, i, (int)((2 + k) * W_FP));
-  r.z.v = ld_fp(p, n, i, (int)((4 + k) * W_FP));
-  return r;
-}
-__device__ __forceinline__ void st_g2jx(uint32_t* p, uint32_t n, uint32_t i, uint32_t k, const g2jx& v) {
-  st_fp(p, n, i, (int)(k * W_FP), v.x.v);
-  st_fp(p, n, i, (int)((2 + k) * W_FP), v.y.v);
-  st_fp(p, n, i, (int)((4 + k) * W_FP), v.z.v);
-}
 // this lane's slot: coordinate c at words c * W_FP .. + 13
 __device__ __forceinline__ g2jx ld_g2jx_slot(const uint32_t* s, uint32_t t) {
   g2jx r;

@@ -15,7 +15,7 @@
 #include "k_common.hpp"
 #include "gt_wave.hpp"
 #include "gt6.hpp"
-#include "fp2x.hpp"
+#include "gtx.hpp"
 
 // Line pairs in the one-lane chunk loop (line_pair + fp12_mul_by_line2: 23 Fp2 products per two items instead of 26):
 // correct (test_line_pair_product, chunk-form GPU parity) but the pending line and the denser product raise the
@@ -284,6 +284,63 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc2(PipelineBuffers b) {
   st_fp2(b.f_chunk, b.n, c, (6 * (int)h + 4) * W_FP, out.c2);
 }
 
+// The accumulation on lane pairs (gtx.hpp): lane 2c + k holds coefficient k of every Fp2 coefficient of chunk c's f
+// (84 registers), so the kernel runs two waves per SIMD; the same chunks as k_miller_acc (K items sharing each
+// squaring), the same work per pairing (25 Fp2 products per doubling step for one-item chunks, 12 / K + 13 for K),
+// each Fp2 product split as two 588-MAD halves.  Each lane loads its coefficients of the lines and scales them by P.
+#ifndef BLSGPU_WPE_ACCX
+#define BLSGPU_WPE_ACCX 2
+#endif
+template <bool UNITS>
+STAGE_KERNEL_W(BLSGPU_WPE_ACCX) void k_miller_accx(PipelineBuffers b) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x;
+  const uint32_t c = q >> 1, k = q & 1;
+  if (c >= b.n_chunks) return;  // whole pairs leave together
+  const uint32_t k0 = b.chunk_first[c], k1 = b.chunk_first[c + 1];
+  fp12x f;
+  f.c0.c0 = F_one((const fp2x*)0);
+  f.c0.c1 = f.c0.c2 = f.c1.c0 = f.c1.c1 = f.c1.c2 = F_zero((const fp2x*)0);
+  int bit = 62;
+  bool add_next = false;
+#pragma unroll 1
+  for (int s = 0; s < MILLER_STEPS; s++) {
+    if (!add_next && s != 0) f = fp12x_sqr(f);
+    const uint32_t* o = b.lines + (size_t)s * W_LINE * b.nm;
+#pragma unroll 1
+    for (uint32_t it = k0; it < k1; it++) {
+      const uint32_t i = b.chunk_items[it];
+      uint32_t m;
+      bool active;
+      if (UNITS) {
+        m = b.unit_msg[i];
+        active = b.unit_ok[i] != 0;
+      } else {
+        m = b.msg_idx[i];
+        active = b.include[i] != 0;
+      }
+      if (!active || (b.mflags[m] & MF_H_INF)) continue;  // the same on both lanes of the pair
+      const g1a P = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
+      const fp2x l0{ld_fp(o, b.nm, m, (int)(k * W_FP))};
+      const fp2x l1{fp_mul(ld_fp(o, b.nm, m, (int)((2 + k) * W_FP)), P.x)};
+      const fp2x l4{fp_mul(ld_fp(o, b.nm, m, (int)((4 + k) * W_FP)), P.y)};
+      f = fp12x_mul_by_014(f, l0, l1, l4);
+    }
+    if (!add_next) {
+      add_next = (BLS_Z_ABS >> bit) & 1ull;
+      bit--;
+    } else {
+      add_next = false;
+    }
+  }
+  // f_chunk[c] = conj(f) = (c0, -c1): lane k writes coefficient k of the six slots
+  st_fp(b.f_chunk, b.n, c, (int)((0 + k) * W_FP), f.c0.c0.v);
+  st_fp(b.f_chunk, b.n, c, (int)((2 + k) * W_FP), f.c0.c1.v);
+  st_fp(b.f_chunk, b.n, c, (int)((4 + k) * W_FP), f.c0.c2.v);
+  st_fp(b.f_chunk, b.n, c, (int)((6 + k) * W_FP), fp_neg(f.c1.c0.v));
+  st_fp(b.f_chunk, b.n, c, (int)((8 + k) * W_FP), fp_neg(f.c1.c1.v));
+  st_fp(b.f_chunk, b.n, c, (int)((10 + k) * W_FP), fp_neg(f.c1.c2.v));
+}
+
 // Mid-size runs (latency): SIX lanes per pairing, lane k of a group holding the w-basis coefficient f_k of
 // f = sum_k f_k w^k (w^6 = xi; tower slots c0.c0, c1.c0, c0.c1, c1.c1, c0.c2, c1.c2), ten groups per wave.  Every lane
 // runs ONE instruction stream (no divergence inside a group): per step
@@ -412,6 +469,13 @@ void launch_miller_acc6(const PipelineBuffers& b, bool units, hipStream_t s) {
     hipLaunchKernelGGL((k_miller_acc6<false, 2>), grid, dim3(WAVE), 0, s, b);
   else
     hipLaunchKernelGGL((k_miller_acc6<false, 1>), grid, dim3(WAVE), 0, s, b);
+}
+void launch_miller_accx(const PipelineBuffers& b, bool units, hipStream_t s) {
+  if (!b.n_chunks) return;
+  if (units)
+    hipLaunchKernelGGL(k_miller_accx<true>, grid_for(2 * b.n_chunks), dim3(WAVE), 0, s, b);
+  else
+    hipLaunchKernelGGL(k_miller_accx<false>, grid_for(2 * b.n_chunks), dim3(WAVE), 0, s, b);
 }
 void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s) {
   if (!b.n_chunks) return;

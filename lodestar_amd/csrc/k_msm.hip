@@ -58,6 +58,55 @@ __global__ __launch_bounds__(MSM_LANES) __attribute__((amdgpu_waves_per_eu(BLSGP
   st_g2j(B, n_slices * MSM_LANES, s * MSM_LANES + t, acc);
 }
 
+// The bucket pass on lane pairs (fp2x.hpp): a 256-lane workgroup per slice, lane pair t / 2 owning bucket (window,
+// e) and lane t holding coefficient t % 2 of its running sum -- half a point per lane, two waves per SIMD.  Both lanes
+// of a pair build the same list (each reads back only what it wrote).
+#ifndef BLSGPU_MSM_PAIRS
+#define BLSGPU_MSM_PAIRS 1
+#endif
+__global__ __launch_bounds__(2 * MSM_LANES) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_msm_bucket2(
+    PipelineBuffers b, const uint32_t* slices, uint32_t n_slices, uint32_t* B) {
+  __shared__ uint64_t sw[MSM_SLICE];
+  __shared__ uint8_t act[MSM_SLICE];
+  __shared__ uint16_t list[2][MSM_WINDOWS][MSM_SLICE];
+  __shared__ uint16_t cnt[MSM_LANES];
+  const uint32_t s = blockIdx.x, t = threadIdx.x, tb = t >> 1, kc = t & 1;
+  if (s >= n_slices) return;
+  const uint32_t first = slices[2 * s], len = slices[2 * s + 1] - first;  // len <= MSM_SLICE (host)
+  for (uint32_t j = t; j < len; j += 2 * MSM_LANES) {
+    const uint32_t i = first + j;
+    act[j] = b.include[i] && !(b.flags[i] & SF_SIG_INF);
+    sw[j] = b.scalars[i];
+  }
+  __syncthreads();
+  const int k = (int)(tb / MSM_BUCKETS);
+  const uint32_t e = tb % MSM_BUCKETS;
+  uint32_t c = 0;
+  for (uint32_t j = 0; j < len; j++) {
+    bool neg;
+    c += (act[j] && msm_bucket(sw[j], k, neg) == e) ? 1u : 0u;
+  }
+  if (kc == 0) cnt[tb] = (uint16_t)c;
+  __syncthreads();
+  uint32_t off = 0;
+  for (uint32_t q = (uint32_t)k * MSM_BUCKETS; q < tb; q++) off += cnt[q];
+  for (uint32_t j = 0, p = off; j < len; j++) {
+    bool neg;
+    if (act[j] && msm_bucket(sw[j], k, neg) == e) list[kc][k][p++] = (uint16_t)(j | (neg ? 0x8000u : 0u));
+  }
+  g2jx acc = jac_infinity<fp2x>();
+#pragma unroll 1
+  for (uint32_t q = 0; q < c; q++) {
+    const uint32_t v = list[kc][k][off + q], i = first + (v & 0x7fffu);
+    aff<fp2x> P;
+    P.x.v = ld_fp(b.sig_aff, b.n, i, (int)(kc * W_FP));
+    P.y.v = ld_fp(b.sig_aff, b.n, i, (int)((2 + kc) * W_FP));
+    if (v & 0x8000u) P.y = F_neg(P.y);
+    acc = jac_add_aff(acc, P);
+  }
+  st_g2jx(B, n_slices * MSM_LANES, s * MSM_LANES + tb, kc, acc);
+}
+
 // One lane per (range, window k, bucket e) -- the 8 lanes of a window are neighbours in one wave.  Range r covers
 // slices [range_slices[r], range_slices[r + 1]); the lane sums its bucket over them (4 slices of a 16k call: 3
 // additions), forms (2e + 1) B_e and the window's lanes sum their terms through LDS in a 3-level tree
@@ -154,7 +203,10 @@ void launch_sig_msm(const PipelineBuffers& b, const uint32_t* slices, uint32_t n
                     uint32_t tree_slices) {
   if (!n_ranges) return;
   if (n_slices) {
-    hipLaunchKernelGGL(k_msm_bucket, dim3(n_slices), dim3(MSM_LANES), 0, st, b, slices, n_slices, B);
+    if (BLSGPU_MSM_PAIRS)
+      hipLaunchKernelGGL(k_msm_bucket2, dim3(n_slices), dim3(2 * MSM_LANES), 0, st, b, slices, n_slices, B);
+    else
+      hipLaunchKernelGGL(k_msm_bucket, dim3(n_slices), dim3(MSM_LANES), 0, st, b, slices, n_slices, B);
   }
   const bool tree = n_slices && tree_slices > 2;
   if (tree)

@@ -2,7 +2,6 @@
 // of the random linear combination (A9), one lane per signature set.
 #include "k_common.hpp"
 #include "g2_coop.hpp"
-#include "fp2x.hpp"
 
 // check_group == false: the subgroup check is left to k_sig_subgroup_coop (small runs) or k_sig_subgroup2 (lane
 // pairs, BLSGPU_SIG_PAIRS); the decode alone then fits two waves per SIMD (WPE_DEC0)

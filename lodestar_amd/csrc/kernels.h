@@ -126,6 +126,7 @@ void launch_miller_lines(const PipelineBuffers& b, hipStream_t s);
 void launch_miller_lines2(const PipelineBuffers& b, hipStream_t s);
 // Miller values of the chunks (items are units when `units`, else sets): f_chunk[c] = prod over the chunk's
 // active items of MillerLoop(P_item, H(m_item)), one lane per chunk, the Fp12 squarings shared
+void launch_miller_accx(const PipelineBuffers& b, bool units, hipStream_t s);
 void launch_miller_acc(const PipelineBuffers& b, bool units, hipStream_t s);
 // the same for chunks of ONE item each, two lanes per pairing (k_miller.hip k_miller_acc2: mid-size runs, latency)
 void launch_miller_acc2(const PipelineBuffers& b, bool units, hipStream_t s);

@@ -209,7 +209,7 @@ struct Options {  // snapshot taken at the start of each call
                                   // MillerLoop(-g1, S) (0 = never)
   int64_t lane_tail_parts = 3;    // bit 0: Horner passes, bit 1: MillerLoop(-g1, S)
   int64_t msm_slice_mid = 32;     // MSM slice length of runs of 1k-32k sets
-  int64_t lines_lanes = 1;        // lanes per message of the Miller lines (1, 2)
+  int64_t lines_lanes = 2;        // lanes per message of the Miller lines (1, or 2 = lane pairs: fp2x.hpp)
   int64_t merge_balance = 0;      // a backlog above merge_sets is cut into equal runs
   int64_t msm_tree = 1;           // those runs sum each range's slices by a pairwise tree
   int64_t coop_max = 512;         // runs of <= this many pairings take the cooperative Miller loops (k_miller_coop)
@@ -219,6 +219,7 @@ struct Options {  // snapshot taken at the start of each call
   int64_t fb_lane_min = 256;      // fallback check launches of >= this many checks take one lane per check (0 = never)
   int64_t route_split_sets = 16384;  // a call is split over min(devices, sets / this) devices, else routed whole
   int64_t acc6_max = 16384;       // one-item-chunk runs of <= this many chunks take the six-lane accumulation
+  int64_t miller_pairs = 0;       // larger runs: the lane-pair accumulation (k_miller_accx, two waves per SIMD)
   int64_t small_max = 4096;       // runs of <= this many sets are latency-first (speculation, cooperative fallback checks)
   int64_t fb_direct_min = 1024;   // large runs under load with >= this many retried jobs check each directly (0 = never)
   int64_t fb_check6 = 2;          // those runs' lane checks: 0 one lane per check; 1 MillerLoop(-g1, S) one lane and the
@@ -232,7 +233,7 @@ struct Options {  // snapshot taken at the start of each call
            msm_slice_mid == o.msm_slice_mid && msm_tree == o.msm_tree &&
            lines_lanes == o.lines_lanes && merge_balance == o.merge_balance && coop_max == o.coop_max &&
            coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec &&
-           fb_lane_min == o.fb_lane_min && acc6_max == o.acc6_max && small_max == o.small_max &&
+           fb_lane_min == o.fb_lane_min && acc6_max == o.acc6_max && miller_pairs == o.miller_pairs && small_max == o.small_max &&
            fb_direct_min == o.fb_direct_min && fb_check6 == o.fb_check6 && fb_force_busy == o.fb_force_busy;
   }
 };
@@ -266,9 +267,13 @@ inline uint32_t miller_k_auto(uint32_t n_items) {
 // acc6_max chunks, two lanes (k_miller_acc2) for larger one-item-chunk runs while one lane per chunk would leave SIMDs
 // idle (< 65,536 chunks = 1,024 waves), else one lane per chunk.
 void launch_miller_acc_auto(const PipelineBuffers& pb, bool units, hipStream_t st, uint32_t mk, int64_t lanes_opt,
-                            int64_t acc6_max) {
+                            int64_t acc6_max, bool pairs) {
   if (lanes_opt == 6 || (lanes_opt == 0 && mk == 1 && (int64_t)pb.n_chunks <= acc6_max)) {
     launch_miller_acc6(pb, units, st);
+    return;
+  }
+  if (lanes_opt == 3 || (lanes_opt == 0 && pairs)) {  // lane pairs, every Fp2 split (gtx.hpp): two waves per SIMD
+    launch_miller_accx(pb, units, st);
     return;
   }
   // two lanes per chunk: f never on one lane, no spills (r4zd/r4ze A/B, PMC r4f); auto: one-item chunks
@@ -851,7 +856,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     beg(kStages, sm);
     if (!coop) {
       // two lanes per message while one lane each would leave SIMDs idle (the same rule as the accumulation's)
-      const bool two = opt.lines_lanes == 2;  // measured: 2.9 ms vs 2.0 ms one-lane at 16k (r4l), lane exchange spills
+      const bool two = opt.lines_lanes == 2;  // lane pairs, two waves per SIMD: C2 +2-4% (profiles/r05_pairs_ab.json)
       if (two)
         launch_miller_lines2(pb, sm);
       else
@@ -910,7 +915,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     if (coop)
       launch_miller_coop(pb, merged, sm, excl);
     else
-      launch_miller_acc_auto(pb, merged, sm, mk, opt.miller_lanes, opt.acc6_max);
+      launch_miller_acc_auto(pb, merged, sm, mk, opt.miller_lanes, opt.acc6_max, opt.miller_pairs != 0);
     end(5, sm);
     if (keep_f)
       HIPCHK(hipMemcpyAsync(sl.d_fkeep.p, pb.f_chunk, (size_t)stride * W_FP12 * 4, hipMemcpyDeviceToDevice, sm));
@@ -1135,7 +1140,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       if (coop)  // no stored lines in a cooperative run: the per-job chunks hold one set each (mk = 1)
         launch_miller_coop(pr, false, sfb);
       else
-        launch_miller_acc_auto(pr, false, sfb, mk, opt.miller_lanes, opt.acc6_max);
+        launch_miller_acc_auto(pr, false, sfb, mk, opt.miller_lanes, opt.acc6_max, opt.miller_pairs != 0);
     }
     st.fallback_jobs += nr;
     if (small_jobs) {
@@ -2028,7 +2033,7 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "serial") {
     ctx->opt.serial = value != 0;
   } else if (k == "miller_lanes") {
-    if (value < 0 || (value > 2 && value != 6)) return BLSGPU_ERR_ARGS;
+    if (value < 0 || (value > 3 && value != 6)) return BLSGPU_ERR_ARGS;
     ctx->opt.miller_lanes = value;
   } else if (k == "msm_slice_mid") {
     if (value < 8 || value > MSM_SLICE) return BLSGPU_ERR_ARGS;
@@ -2065,6 +2070,9 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "small_max") {
     if (value < 0) return BLSGPU_ERR_ARGS;
     ctx->opt.small_max = value;
+  } else if (k == "miller_pairs") {
+    if (value < 0 || value > 1) return BLSGPU_ERR_ARGS;
+    ctx->opt.miller_pairs = value;
   } else if (k == "acc6_max") {
     if (value < 0) return BLSGPU_ERR_ARGS;
     ctx->opt.acc6_max = value;
@@ -2136,6 +2144,7 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "fb_lane_min") *value = o.fb_lane_min;
   else if (k == "route_split_sets") *value = o.route_split_sets;
   else if (k == "acc6_max") *value = o.acc6_max;
+  else if (k == "miller_pairs") *value = o.miller_pairs;
   else if (k == "small_max") *value = o.small_max;
   else if (k == "fb_direct_min") *value = o.fb_direct_min;
   else if (k == "fb_check6") *value = o.fb_check6;

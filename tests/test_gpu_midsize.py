@@ -89,6 +89,7 @@ def test_midsize_one_percent_corrupt_vs_oracle(ctx, pool, n):
     {"fb_lane_min": 1, "coop_max": 0},              # lane-per-check fallback checks (merged runs under load)
     {"coop_max": 0, "acc6_max": 0},                 # two-lane accumulation instead of the six-lane one
     {"coop_max": 0, "miller_lanes": 6, "dedupe": 0},  # six lanes forced
+    {"coop_max": 0, "miller_lanes": 3},               # lane pairs (gtx.hpp) for the batch pass and the fallback
     # the fallback's under-load forms: one-lane MillerLoop(-g1, S) + six-lane final exponentiations (gt6.hpp), per job
     # directly or after sub-groups; and the all-one-lane checks
     {"fb_force_busy": 1, "fb_direct_min": 1, "fb_lane_min": 1},
@@ -109,11 +110,21 @@ def test_midsize_forms_agree(ctx, pool, opts):
             ctx.set_option(k, v)
 
 
-def test_fallback_units_recompute_vs_oracle(ctx, pool):
+@pytest.mark.parametrize("lanes", [0, 3])
+def test_fallback_units_recompute_vs_oracle(ctx, pool, lanes):
     """Same-message units (4 sets per root): the batch pass pairs units, not sets, so the fallback recomputes the
-    failed jobs' Miller loops (fallback_miller > 0) -- still job for job equal to the oracle."""
+    failed jobs' Miller loops (fallback_miller > 0) -- still job for job equal to the oracle (default Miller forms, and
+    lane pairs for every accumulation)."""
     call, _ = make_call(pool, 2048, 0x7000, share_every=4)
-    got, st = compare(ctx, call)
+    saved = (ctx.get_option("miller_lanes"), ctx.get_option("coop_max"))
+    ctx.set_option("miller_lanes", lanes)
+    if lanes:
+        ctx.set_option("coop_max", 0)
+    try:
+        got, st = compare(ctx, call)
+    finally:
+        ctx.set_option("miller_lanes", saved[0])
+        ctx.set_option("coop_max", saved[1])
     assert st.fallback_jobs > 0 and st.fallback_miller > 0
 
 

@@ -436,10 +436,11 @@ def test_merged_run_isolates_bad_call():
         c.close()
 
 
-@pytest.mark.parametrize("k,lanes", [(2, 2), (4, 2), (2, 1), (1, 1), (1, 6), (2, 6), (3, 6)])
+@pytest.mark.parametrize("k,lanes", [(2, 2), (4, 2), (2, 1), (1, 1), (1, 6), (2, 6), (3, 6), (1, 3), (2, 3), (3, 3)])
 def test_miller_chunk_forms_vs_oracle(ctx, k, lanes):
     """The Miller accumulation's chunk forms: chunks of k pairings on six lanes (one w-basis coefficient of f each),
-    two lanes (halves of f, the squaring shared by the chunk) or one lane, forced on a 2,048-set call with ~1% corrupted
+    two lanes (halves of f, the squaring shared by the chunk), lane pairs (lanes 3: every Fp2 split, gtx.hpp) or one
+    lane, forced on a 2,048-set call with ~1% corrupted
     sets (so the fallback re-checks jobs through the same kernels): job for job equal to the oracle.  (coop_max 0: the
     lane forms even for a run this small.)"""
     n = 2048
@@ -502,16 +503,18 @@ def test_balanced_merging_keeps_answers():
         c.close()
 
 
-def test_two_lane_lines_vs_oracle(ctx):
-    """The two-lanes-per-message Miller lines (k_miller_lines2, lines_lanes 2) on a 2,048-set call with ~1% corrupted
-    sets: job for job equal to the oracle."""
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_two_lane_lines_vs_oracle(ctx, lanes):
+    """The Miller lines on one lane per message (k_miller_lines) and on lane pairs (k_miller_lines2, fp2x.hpp; the
+    default lines_lanes 2) on a 2,048-set call with ~1% corrupted sets: job for job equal to the oracle."""
     n = 2048
     rng = np.random.default_rng(99)
     sks, pks, msgs, sigs, sig_len = corrupted_single_sets(n, b"L2", rng)
     base = dict(sigs=sigs, sig_len=sig_len, msgs=b"".join(msgs), sig_stride=192)
-    ctx.set_option("lines_lanes", 2)
+    saved = ctx.get_option("lines_lanes")
+    ctx.set_option("lines_lanes", lanes)
     try:
         got, st = compare(ctx, job_first_set=np.arange(n + 1), pk_bytes=pks, job_flags=np.ones(n), **base)
     finally:
-        ctx.set_option("lines_lanes", 1)
+        ctx.set_option("lines_lanes", saved)
     assert (got == 1).sum() >= n - max(8, n // 100)
