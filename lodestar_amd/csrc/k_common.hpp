@@ -27,8 +27,13 @@ static_assert(2 * WAVE <= BLS_FP2_LDS_LANES, "128-lane kernels (gt_wave.hpp, k_m
 // Per-kernel register budgets (waves per SIMD), default BLSGPU_WPE: a kernel whose live state fits 256 registers
 // with little spilling can take two waves per SIMD, so two waves hide each other's dependent-MAD latency.
 #define STAGE_KERNEL_W(w) __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(w, w)))
+// k_pk_finish at two waves (256 registers, 368 B scratch): C2 within noise, C4 2.42M -> 2.16M (r05aa): one wave
 #ifndef BLSGPU_WPE_PK
 #define BLSGPU_WPE_PK BLSGPU_WPE
+#endif
+// k_hash_prep at two waves: C2 within noise, slightly lower (3.72M vs 3.77M, three rounds of 100 steps): one wave
+#ifndef BLSGPU_WPE_HPREP
+#define BLSGPU_WPE_HPREP 1
 #endif
 #ifndef BLSGPU_WPE_MSM
 #define BLSGPU_WPE_MSM BLSGPU_WPE

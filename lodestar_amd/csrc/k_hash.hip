@@ -12,29 +12,6 @@
 #define BLSGPU_HASH_PAIRS 1
 #endif
 
-__device__ __forceinline__ void st_prep(uint32_t* p, uint32_t n, uint32_t u, const h2c_prep& h) {
-  st_fp2(p, n, u, 0 * W_FP, h.u0);
-  st_fp2(p, n, u, 2 * W_FP, h.u1);
-  st_fp2(p, n, u, 4 * W_FP, h.Zu2_0);
-  st_fp2(p, n, u, 6 * W_FP, h.Zu2_1);
-  st_fp2(p, n, u, 8 * W_FP, h.tv0);
-  st_fp2(p, n, u, 10 * W_FP, h.tv1);
-  st_fp2(p, n, u, 12 * W_FP, h.d);
-}
-STAGE_KERNEL void k_hash_prep(PipelineBuffers b) {
-  uint32_t u = blockIdx.x * WAVE + threadIdx.x;
-  if (u >= b.n_umsg) return;
-  uint8_t msg[32];
-  const uint4* src = reinterpret_cast<const uint4*>(b.umsgs + (size_t)u * 32);
-  uint4 m0 = src[0], m1 = src[1];
-  uint32_t w[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
-#pragma unroll
-  for (int k = 0; k < 32; k++) msg[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-  h2c_prep h;
-  hash_to_g2_prep(msg, h);
-  st_prep(b.h_prep, b.nm, u, h);
-  st_fp(b.h_norm, b.nm, u, 0, fp2_norm(h.d));
-}
 
 // Q = q0 + q1, cofactor clearing (RFC 9380 G.3); Jacobian out + N(z) for the batched affine conversion.  The
 // clearing (clear_cofactor_g2_slots) keeps the base point of each [|z|] chain -- Q, then A - psi(Q) -- in this lane's
@@ -165,7 +142,7 @@ static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
 void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s, bool coop, bool exclusive) {
   if (!b.n_umsg) return;
-  hipLaunchKernelGGL(k_hash_prep, grid_for(b.n_umsg), dim3(WAVE), 0, s, b);
+  launch_hash_prep(b, s);
   launch_batch_inv(b.h_norm, b.nm, 0, b.inv_buf, b.n_umsg, s);
   launch_hash_map(b, b.inv_buf, s);
   if (coop)

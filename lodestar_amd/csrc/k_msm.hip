@@ -64,6 +64,11 @@ __global__ __launch_bounds__(MSM_LANES) __attribute__((amdgpu_waves_per_eu(BLSGP
 #ifndef BLSGPU_MSM_PAIRS
 #define BLSGPU_MSM_PAIRS 1
 #endif
+// The window sums and the slice tree on lane pairs too: C2 within noise (3.72M vs 3.72M, three rounds of 100 steps),
+// the isolated 16k call's MSM slower (3.7-4.2 vs 1.7-3.1 ms): off
+#ifndef BLSGPU_MSM_WPAIRS
+#define BLSGPU_MSM_WPAIRS 0
+#endif
 __global__ __launch_bounds__(2 * MSM_LANES) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_msm_bucket2(
     PipelineBuffers b, const uint32_t* slices, uint32_t n_slices, uint32_t* B) {
   __shared__ uint64_t sw[MSM_SLICE];
@@ -126,6 +131,19 @@ STAGE_KERNEL void k_msm_slice_pairs(const uint32_t* range_slices, uint32_t n_ran
   st_g2j(B, nb, a * MSM_LANES + tb, jac_add(ld_g2j(B, nb, a * MSM_LANES + tb), ld_g2j(B, nb, c * MSM_LANES + tb)));
 }
 
+// the same level on lane pairs (fp2x.hpp)
+STAGE_KERNEL_W(2) void k_msm_slice_pairs2(const uint32_t* range_slices, uint32_t n_ranges, uint32_t* B,
+                                          uint32_t n_slices, uint32_t stride, uint32_t max_pairs) {
+  const uint32_t q2 = blockIdx.x * WAVE + threadIdx.x, q = q2 >> 1, kc = q2 & 1;
+  const uint32_t tb = q % MSM_LANES, rest = q / MSM_LANES, j = rest % max_pairs, r = rest / max_pairs;
+  if (r >= n_ranges) return;
+  const uint32_t s0 = range_slices[r], s1 = range_slices[r + 1], a = s0 + 2 * j * stride, c = a + stride;
+  if (c >= s1) return;
+  const uint32_t nb = n_slices * MSM_LANES;
+  st_g2jx(B, nb, a * MSM_LANES + tb, kc,
+          jac_add(ld_g2jx(B, nb, a * MSM_LANES + tb, kc), ld_g2jx(B, nb, c * MSM_LANES + tb, kc)));
+}
+
 STAGE_KERNEL void k_msm_window(const uint32_t* range_slices, uint32_t n_ranges, const uint32_t* B, uint32_t n_slices,
                                uint32_t* W, bool presummed) {
   __shared__ uint32_t xch[W_G2J * WAVE];
@@ -150,6 +168,44 @@ STAGE_KERNEL void k_msm_window(const uint32_t* range_slices, uint32_t n_ranges, 
     __syncthreads();
   }
   if (on && e == 0) st_g2j(W, n_ranges * MSM_WINDOWS, q / MSM_BUCKETS, T);
+}
+
+// The window sums on lane pairs (fp2x.hpp): lane pair q / 2 per (range, window, bucket), lane q holding coefficient
+// q % 2; the window's 16 lanes sum their terms through LDS in the same 3-level tree.
+STAGE_KERNEL_W(2) void k_msm_window2(const uint32_t* range_slices, uint32_t n_ranges, const uint32_t* B,
+                                     uint32_t n_slices, uint32_t* W, bool presummed) {
+  __shared__ uint32_t xch[3 * W_FP * WAVE];
+  const uint32_t t = threadIdx.x, q = blockIdx.x * WAVE + t, qb = q >> 1, kc = q & 1;
+  const bool on = qb < n_ranges * MSM_LANES;
+  const uint32_t r = qb / MSM_LANES, tb = qb % MSM_LANES, e = tb % MSM_BUCKETS;
+  g2jx T = jac_infinity<fp2x>();
+  if (on) {
+    const uint32_t s0 = range_slices[r], s1 = presummed ? std::min(range_slices[r + 1], s0 + 1) : range_slices[r + 1],
+                   nb = n_slices * MSM_LANES;
+    if (s0 < s1) T = ld_g2jx(B, nb, s0 * MSM_LANES + tb, kc);
+#pragma unroll 1
+    for (uint32_t s = s0 + 1; s < s1; s++) T = jac_add(T, ld_g2jx(B, nb, s * MSM_LANES + tb, kc));
+    T = msm_odd_multiple(T, e);
+  }
+  static_assert(WAVE % (2 * MSM_BUCKETS) == 0, "a window's lane pairs share a workgroup");
+#pragma unroll 1
+  for (uint32_t h = 1; h < MSM_BUCKETS; h <<= 1) {
+    if ((e & (2 * h - 1)) == h) {
+      st_fp(xch, WAVE, t, 0, T.x.v);
+      st_fp(xch, WAVE, t, W_FP, T.y.v);
+      st_fp(xch, WAVE, t, 2 * W_FP, T.z.v);
+    }
+    __syncthreads();
+    if ((e & (2 * h - 1)) == 0) {
+      g2jx o;
+      o.x.v = ld_fp(xch, WAVE, t + 2 * h, 0);
+      o.y.v = ld_fp(xch, WAVE, t + 2 * h, W_FP);
+      o.z.v = ld_fp(xch, WAVE, t + 2 * h, 2 * W_FP);
+      T = jac_add(T, o);
+    }
+    __syncthreads();
+  }
+  if (on && e == 0) st_g2jx(W, n_ranges * MSM_WINDOWS, qb / MSM_BUCKETS, kc, T);
 }
 
 // Horner passes on cooperative 16-lane groups (g2_coop.hpp): a workgroup of 128 lanes runs 4 ranges, group 2j the
@@ -212,11 +268,19 @@ void launch_sig_msm(const PipelineBuffers& b, const uint32_t* slices, uint32_t n
   if (tree)
     for (uint32_t stride = 1; stride < tree_slices; stride *= 2) {
       const uint32_t max_pairs = (tree_slices + 2 * stride - 1) / (2 * stride);
-      hipLaunchKernelGGL(k_msm_slice_pairs, grid_for(n_ranges * max_pairs * MSM_LANES), dim3(WAVE), 0, st,
-                         range_slices, n_ranges, B, n_slices, stride, max_pairs);
+      if (BLSGPU_MSM_WPAIRS)
+        hipLaunchKernelGGL(k_msm_slice_pairs2, grid_for(2 * n_ranges * max_pairs * MSM_LANES), dim3(WAVE), 0, st,
+                           range_slices, n_ranges, B, n_slices, stride, max_pairs);
+      else
+        hipLaunchKernelGGL(k_msm_slice_pairs, grid_for(n_ranges * max_pairs * MSM_LANES), dim3(WAVE), 0, st,
+                           range_slices, n_ranges, B, n_slices, stride, max_pairs);
     }
-  hipLaunchKernelGGL(k_msm_window, grid_for(n_ranges * MSM_LANES), dim3(WAVE), 0, st, range_slices, n_ranges, B,
-                     n_slices, W, tree);
+  if (BLSGPU_MSM_WPAIRS)
+    hipLaunchKernelGGL(k_msm_window2, grid_for(2 * n_ranges * MSM_LANES), dim3(WAVE), 0, st, range_slices, n_ranges, B,
+                       n_slices, W, tree);
+  else
+    hipLaunchKernelGGL(k_msm_window, grid_for(n_ranges * MSM_LANES), dim3(WAVE), 0, st, range_slices, n_ranges, B,
+                       n_slices, W, tree);
   if (lane_tail)
     hipLaunchKernelGGL(k_msm_horner_lane, grid_for(2 * n_ranges), dim3(WAVE), 0, st, W, n_ranges, S);
   else

@@ -91,6 +91,7 @@ void launch_sig_decode(const PipelineBuffers& b, uint32_t n_sets, hipStream_t s,
                        hipEvent_t decoded = nullptr, bool exclusive = true);
 // spec[i] = the signature of set i decoded (the speculative MSM's include mask)
 void launch_spec_mask(const PipelineBuffers& b, uint32_t n_sets, uint8_t* spec, hipStream_t s);
+void launch_hash_prep(const PipelineBuffers& b, hipStream_t s);
 void launch_hash_map(const PipelineBuffers& b, const uint32_t* inv, hipStream_t s);
 void launch_hash_to_g2(const PipelineBuffers& b, hipStream_t s, bool coop = false,
                        bool exclusive = true);  // over the unique messages

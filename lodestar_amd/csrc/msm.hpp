@@ -36,9 +36,10 @@ BLS_HD uint32_t msm_bucket(uint64_t w, int k, bool& neg) {
 // W = sum_e (2e + 1) B_e on 8 lanes (k_msm_window): lane e forms (2e + 1) B_e with one chain for every lane (bits of e from the
 // top, the addend T or infinity, so the wave does not diverge: 3 doublings + 3 additions), then a 3-level tree sums
 // the 8 terms -- 6 additions deep instead of the 18 of running sums.
-BLS_INL g2j msm_odd_multiple(const g2j& T, uint32_t e) {
-  const g2j inf = jac_infinity<fp2>();
-  g2j R = (e & 4u) ? T : inf;
+template <class F>
+BLS_INL jac<F> msm_odd_multiple(const jac<F>& T, uint32_t e) {
+  const jac<F> inf = jac_infinity<F>();
+  jac<F> R = (e & 4u) ? T : inf;
   R = jac_add(jac_dbl(R), (e & 2u) ? T : inf);
   R = jac_add(jac_dbl(R), (e & 1u) ? T : inf);
   return jac_add(jac_dbl(R), T);
