@@ -20,6 +20,7 @@
 // There is no CPU verification path: without a usable GPU blsgpu_init fails.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/random.h>
@@ -54,6 +55,9 @@ struct HipError {
 // Device buffer that only grows.  A slot's buffers grow stream-ordered (hipFreeAsync / hipMallocAsync on the
 // slot's stream): a plain hipFree waits for the whole device, so a merged run larger than any before would stall
 // every other slot's work (seen as 1.4-2.5 s call latencies in the bench's tail).  Growth doubles.
+// growths of stream-ordered slot buffers by this thread (run_shard: an input copy may leave the run's stream only when
+// no buffer of the run was (re)allocated in that stream's order)
+thread_local uint64_t tl_async_grow = 0;
 template <class T>
 struct DevBuf {
   T* p = nullptr;
@@ -66,6 +70,7 @@ struct DevBuf {
       if (p) HIPCHK(hipFreeAsync(p, st));
       p = nullptr;
       HIPCHK(hipMallocAsync((void**)&p, c * sizeof(T), st));
+      tl_async_grow++;
     } else {
       if (p) HIPCHK(hipFree(p));
       p = nullptr;
@@ -211,6 +216,9 @@ struct Options {  // snapshot taken at the start of each call
   int64_t msm_slice_mid = 32;     // MSM slice length of runs of 1k-32k sets
   int64_t lines_lanes = 2;        // lanes per message of the Miller lines (1, or 2 = lane pairs: fp2x.hpp)
   int64_t merge_balance = 0;      // a backlog above merge_sets is cut into equal runs
+  int64_t early_release = 0;      // a run leaves the pipeline count when its message branch is done
+  int64_t tail_on_msg = 0;        // the group stage runs on the pair's high-priority message stream
+  int64_t copy_stream = 0;        // a run's input copy on the table stream (not behind the pair's previous tail)
   int64_t msm_tree = 1;           // those runs sum each range's slices by a pairwise tree
   int64_t coop_max = 512;         // runs of <= this many pairings take the cooperative Miller loops (k_miller_coop)
   int64_t coop_g2_max = 4096;     // runs of <= this many sets take the cooperative [|z|] chains (clearing, subgroup)
@@ -231,7 +239,7 @@ struct Options {  // snapshot taken at the start of each call
            f_run_max == o.f_run_max && lane_tail_min == o.lane_tail_min &&
            lane_tail_parts == o.lane_tail_parts &&
            msm_slice_mid == o.msm_slice_mid && msm_tree == o.msm_tree &&
-           lines_lanes == o.lines_lanes && merge_balance == o.merge_balance && coop_max == o.coop_max &&
+           lines_lanes == o.lines_lanes && merge_balance == o.merge_balance && early_release == o.early_release && tail_on_msg == o.tail_on_msg && copy_stream == o.copy_stream && coop_max == o.coop_max &&
            coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec &&
            fb_lane_min == o.fb_lane_min && acc6_max == o.acc6_max && miller_pairs == o.miller_pairs && small_max == o.small_max &&
            fb_direct_min == o.fb_direct_min && fb_check6 == o.fb_check6 && fb_force_busy == o.fb_force_busy;
@@ -450,6 +458,21 @@ struct MsgIndex {
 // Runs one device's shard on one slot.  Writes job_result[job_begin..job_end).
 // A slot's run leaves the device's in-flight count (once): its batch pass is complete on the GPU, so another slot
 // may start the next run while this one finishes on the host (results, fallback round trips).
+// Host-side timing of run formation (diagnostics): BLSGPU_HOST_TRACE=1 prints, per run, the milliseconds spent
+// merging calls, in the host prep before the input copy, and in total before the batch pass is queued.
+static bool host_trace() {
+  static const bool on = [] {
+    const char* v = getenv("BLSGPU_HOST_TRACE");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+static double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+thread_local std::chrono::steady_clock::time_point tl_run_t0;
+thread_local double tl_merge_ms = 0;
+
 void release_inflight(Device& d, Slot& sl) {
   {
     std::lock_guard<std::mutex> lk(d.q_mu);
@@ -472,6 +495,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   const uint32_t nj = sh.job_end - sh.job_begin;
   if (nj == 0) return BLSGPU_OK;
   HIPCHK(hipSetDevice(d.id));
+  const auto t_prep0 = std::chrono::steady_clock::now();
+  const uint64_t grow0 = tl_async_grow;
   const uint32_t s0 = sh.set_begin;
   const uint32_t stride = std::max<uint32_t>(n, 1);
   const bool table_mode = b.pk_bytes == nullptr;
@@ -844,8 +869,17 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   };
   {
     std::lock_guard<std::mutex> enq(d.enq_mu);
-    HIPCHK(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, s));
-    HIPCHK(hipEventRecord(sl.join_in, s));
+    if (host_trace())
+      fprintf(stderr, "[blsgpu host] run %u sets: merge %.2f ms, prep %.2f ms, pick-to-copy %.2f ms, %zu B in\n", n,
+              tl_merge_ms, ms_since(t_prep0), ms_since(tl_run_t0), in_bytes);
+    // The input copy goes on the run's signature stream, or (copy_stream, when none of the run's buffers was
+    // reallocated in that stream's order) on the device's table stream: a previous run's tail still queued on the
+    // signature stream of this pair then delays only this run's signature branch, not its message branch
+    const bool own_copy = opt.copy_stream && !opt.serial && tl_async_grow == grow0;
+    hipStream_t sc = own_copy ? d.table_stream : s;
+    HIPCHK(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, sc));
+    HIPCHK(hipEventRecord(sl.join_in, sc));
+    if (own_copy) HIPCHK(hipStreamWaitEvent(s, sl.join_in, 0));
     HIPCHK(hipStreamWaitEvent(sm, sl.join_in, 0));
     HIPCHK(hipStreamWaitEvent(sp, sl.join_in, 0));
     // messages
@@ -931,12 +965,22 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       launch_sig_msm(pb, d_slices, n_slices, d_rslices, ng0, sl.d_msmB.p, sl.d_msmW.p, sl.d_S.p, s,
                      lane_tail && (opt.lane_tail_parts & 1), msm_tree);
     end(4, s);
-    // MillerLoop(-g1, S_g) of every group now, while the message branch still runs
-    beg(kStages + 1, s);
-    launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, s, excl && coop,
+    // MillerLoop(-g1, S_g) of every group now, while the message branch still runs -- or (tail_on_msg) after it, on
+    // the pair's high-priority message stream with the final exponentiations: a run's cooperative tail kernels then
+    // take free SIMDs before the next runs' stage kernels, and they never hold the signature stream the next run on
+    // this pair copies its inputs on
+    const bool tail_msg = opt.tail_on_msg && !opt.serial && BLSGPU_STREAM_PAIRS;
+    hipStream_t sg = s;
+    if (tail_msg) {
+      HIPCHK(hipEventRecord(sl.join_gsm, s));
+      HIPCHK(hipStreamWaitEvent(sm, sl.join_gsm, 0));
+      sg = stl = sm;
+    }
+    beg(kStages + 1, sg);
+    launch_group_sig_miller(sl.d_S.p, ng0, sl.d_G.p, sg, excl && coop,
                             lane_tail && (opt.lane_tail_parts & 2));
-    end(kStages + 1, s);
-    HIPCHK(hipEventRecord(sl.join_gsm, s));
+    end(kStages + 1, sg);
+    HIPCHK(hipEventRecord(sl.join_gsm, sg));
     HIPCHK(hipStreamWaitEvent(stl, sl.join_gsm, 0));
     HIPCHK(hipStreamWaitEvent(stl, sl.join_msg, 0));
     if (rsig_spec) HIPCHK(hipStreamWaitEvent(stl, sl.join_rsig, 0));  // the run completes with its r_i sig_i
@@ -946,6 +990,13 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(sl.h_res.p, sl.d_res.p, o_ok + ng0, hipMemcpyDeviceToHost, stl));
     HIPCHK(hipEventRecord(sl.done, stl));
+  }
+  if (opt.early_release && !opt.serial) {
+    // the run leaves the in-flight count once its message branch is done: its remaining tail (the signature side's
+    // window sums / Horner / MillerLoop(-g1, S) and the final exponentiations) is short on a chip with room and must
+    // not hold a pipeline place while the next runs' heavy kernels starve it
+    HIPCHK(hipEventSynchronize(sl.join_msg));
+    release_inflight(d, sl);
   }
   HIPCHK(hipEventSynchronize(sl.done));
   if (batch_rand::take_injection(g_fail_run_skip, g_fail_run_count)) throw HipError{hipErrorLaunchFailure};
@@ -1427,6 +1478,7 @@ inline bool table_covers(const Device& d, const Call* c, const Shard& sh) {
 // joins the run; a failure of the run completes its calls with DEVICE_ERROR (every job rejected, never `false`).
 // The caller holds the device's table lock (shared).
 void run_merged(Device& d, Slot& sl, const std::vector<Task>& parts, std::vector<int>& rcs) {
+  const auto t_merge0 = std::chrono::steady_clock::now();
   std::vector<size_t> live;
   for (size_t p = 0; p < parts.size(); p++) {
     const Call* c = parts[p].call;
@@ -1509,6 +1561,7 @@ void run_merged(Device& d, Slot& sl, const std::vector<Task>& parts, std::vector
     mb.sig_stride = 192;
     res.assign(std::max<uint32_t>(nj, 1), 0);
     const Shard all{0, nj, 0, n};
+    tl_merge_ms = ms_since(t_merge0);
     rc = run_call_shard(d, sl, mb, all, res.data(), c0->seed, c0->opt, max_index, st, scal.data());
   } catch (...) {
     rc = BLSGPU_DEVICE_ERROR;
@@ -1640,6 +1693,8 @@ void worker_loop(Device* d, Slot* sl) {
       d->runs_inflight++;
       sl->in_flight = true;
     }
+    tl_run_t0 = std::chrono::steady_clock::now();
+    tl_merge_ms = 0;
     struct InflightGuard {  // the run leaves the in-flight count when its batch pass completes (run_shard) or here
       Device* d;
       Slot* sl;
@@ -2038,6 +2093,12 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   } else if (k == "msm_slice_mid") {
     if (value < 8 || value > MSM_SLICE) return BLSGPU_ERR_ARGS;
     ctx->opt.msm_slice_mid = value;
+  } else if (k == "copy_stream") {
+    ctx->opt.copy_stream = value != 0;
+  } else if (k == "tail_on_msg") {
+    ctx->opt.tail_on_msg = value != 0;
+  } else if (k == "early_release") {
+    ctx->opt.early_release = value != 0;
   } else if (k == "merge_balance") {
     ctx->opt.merge_balance = value != 0;
   } else if (k == "lines_lanes") {
@@ -2137,6 +2198,9 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "msm_tree") *value = o.msm_tree;
   else if (k == "lines_lanes") *value = o.lines_lanes;
   else if (k == "merge_balance") *value = o.merge_balance;
+  else if (k == "early_release") *value = o.early_release;
+  else if (k == "tail_on_msg") *value = o.tail_on_msg;
+  else if (k == "copy_stream") *value = o.copy_stream;
   else if (k == "coop_max") *value = o.coop_max;
   else if (k == "coop_g2_max") *value = o.coop_g2_max;
   else if (k == "coop_excl_max") *value = o.coop_excl_max;
