@@ -436,12 +436,17 @@ struct MsgIndex {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
   }
-  // returns the unique index of msg; appends to `uniq` (set indices of first occurrences) when new
-  uint32_t find_or_add(const uint8_t* msgs, uint32_t i, std::vector<uint32_t>& uniq) {
+  size_t hash(const uint8_t* msgs, uint32_t i) const {
     uint64_t w[4];
     memcpy(w, msgs + (size_t)i * 32, 32);
+    return (size_t)(mix(w[0] ^ key) ^ mix(w[1] + key) ^ w[2] ^ (w[3] << 1)) & (slot.size() - 1);
+  }
+  // returns the unique index of msg; appends to `uniq` (set indices of first occurrences) when new
+  uint32_t find_or_add(const uint8_t* msgs, uint32_t i, std::vector<uint32_t>& uniq) {
+    return find_or_add_h(msgs, i, hash(msgs, i), uniq);
+  }
+  uint32_t find_or_add_h(const uint8_t* msgs, uint32_t i, size_t h, std::vector<uint32_t>& uniq) {
     const size_t mask = slot.size() - 1;
-    size_t h = (size_t)(mix(w[0] ^ key) ^ mix(w[1] + key) ^ w[2] ^ (w[3] << 1)) & mask;
     for (;;) {
       const uint32_t s = slot[h];
       if (!s) {
@@ -558,13 +563,30 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   if (opt.dedupe) {
     MsgIndex mi(n, seed ^ 0x6a09e667f3bcc908ull);
     uniq.reserve(n);
-    for (uint32_t i = 0; i < n; i++) msg_idx[i] = mi.find_or_add(b.msgs + (size_t)s0 * 32, i, uniq);
+    // hashes a few sets ahead, their table slots prefetched: the probes of a 131k-set run's 1 MB table were cache
+    // misses one after another (~1.3-2.6 ms per run on the host)
+    const uint8_t* ms = b.msgs + (size_t)s0 * 32;
+    constexpr uint32_t kAhead = 16;
+    size_t hq[kAhead];
+    for (uint32_t i = 0; i < std::min(n, kAhead); i++) {
+      hq[i] = mi.hash(ms, i);
+      __builtin_prefetch(&mi.slot[hq[i]]);
+    }
+    for (uint32_t i = 0; i < n; i++) {
+      const size_t h = hq[i % kAhead];
+      if (i + kAhead < n) {
+        hq[i % kAhead] = mi.hash(ms, i + kAhead);
+        __builtin_prefetch(&mi.slot[hq[i % kAhead]]);
+      }
+      msg_idx[i] = mi.find_or_add_h(ms, i, h, uniq);
+    }
   } else {
     uniq.resize(n);
     for (uint32_t i = 0; i < n; i++) msg_idx[i] = uniq[i] = i;
   }
   const uint32_t n_umsg = (uint32_t)uniq.size();
   const uint32_t nm = std::max<uint32_t>(n_umsg, 1);
+  const double t_dedupe_ms = host_trace() ? ms_since(t_prep0) : 0;
   // units: within each group, one unit per distinct message
   std::vector<uint32_t> unit_of_set(n, UINT32_MAX), unit_msg, unit_first, unit_sets, g_unit_first(ng0 + 1, 0);
   bool merged = false;
@@ -695,8 +717,16 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // ---- stage inputs in the pinned arena and copy it to the device in one transfer ------------------------
   // arena (256-B aligned sections): scalars | job_first_set | sigs (192 B each) | sig_len | unique msgs |
   // msg_idx | set ranges | f ranges | units (first, sets, msg) | chunks | agg sets | MSM slices | F tree | pk section
+  const double t_struct_ms = host_trace() ? ms_since(t_prep0) : 0;
+  // signatures at a 96-byte stride when no set carries a 192-byte (uncompressed) one: half the staging and copy
+  uint32_t sig_w = 96;
+  for (uint32_t i = 0; i < n; i++)
+    if (b.sig_len[s0 + i] == 192) {
+      sig_w = 192;
+      break;
+    }
   const size_t o_scal = 0, o_jobs = al256(o_scal + (size_t)n * 8), o_sigs = al256(o_jobs + (size_t)(nj + 1) * 4),
-               o_siglen = al256(o_sigs + (size_t)n * 192), o_umsg = al256(o_siglen + (size_t)n * 4),
+               o_siglen = al256(o_sigs + (size_t)n * sig_w), o_umsg = al256(o_siglen + (size_t)n * 4),
                o_midx = al256(o_umsg + (size_t)n_umsg * 32), o_ranges = al256(o_midx + (size_t)n * 4),
                o_franges = al256(o_ranges + (size_t)std::max(ng0, 1u) * 8),
                o_ufirst = al256(o_franges + (size_t)std::max(ng0, 1u) * 8),
@@ -725,11 +755,16 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   hjobs[nj] = n;
   uint8_t* hsigs = hin + o_sigs;
   uint32_t* hsiglen = reinterpret_cast<uint32_t*>(hin + o_siglen);
-  for (uint32_t i = 0; i < n; i++) {
-    const uint32_t len = b.sig_len[s0 + i];
-    const uint32_t cl = (len == 96 || len == 192) ? len : 0;
-    memcpy(hsigs + (size_t)i * 192, b.sigs + (size_t)(s0 + i) * b.sig_stride, cl);
-    hsiglen[i] = len;
+  if (b.sig_stride == sig_w) {  // one block (the decoder reads only the bytes a set's length makes valid)
+    memcpy(hsigs, b.sigs + (size_t)s0 * sig_w, (size_t)n * sig_w);
+    memcpy(hsiglen, b.sig_len + s0, (size_t)n * 4);
+  } else {
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t len = b.sig_len[s0 + i];
+      const uint32_t cl = (len == 96 || len == 192) ? len : 0;
+      memcpy(hsigs + (size_t)i * sig_w, b.sigs + (size_t)(s0 + i) * b.sig_stride, cl);
+      hsiglen[i] = len;
+    }
   }
   for (uint32_t u = 0; u < n_umsg; u++) memcpy(hin + o_umsg + (size_t)u * 32, b.msgs + (size_t)(s0 + uniq[u]) * 32, 32);
   memcpy(hin + o_midx, msg_idx.data(), (size_t)n * 4);
@@ -792,7 +827,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   pb.n = stride;
   pb.sigs = din + o_sigs;
   pb.sig_len = reinterpret_cast<uint32_t*>(din + o_siglen);
-  pb.sig_stride = 192;
+  pb.sig_stride = sig_w;
   pb.pk_bytes = table_mode ? nullptr : din + (bytes_agg ? o_pk2 : o_pk);
   pb.set_pk_first = (table_mode || bytes_agg) ? reinterpret_cast<uint32_t*>(din + o_pk) : nullptr;
   pb.pk_index = table_mode ? reinterpret_cast<uint32_t*>(din + o_pk2) : nullptr;
@@ -870,8 +905,10 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   {
     std::lock_guard<std::mutex> enq(d.enq_mu);
     if (host_trace())
-      fprintf(stderr, "[blsgpu host] run %u sets: merge %.2f ms, prep %.2f ms, pick-to-copy %.2f ms, %zu B in\n", n,
-              tl_merge_ms, ms_since(t_prep0), ms_since(tl_run_t0), in_bytes);
+      fprintf(stderr,
+              "[blsgpu host] run %u sets: merge %.2f ms, prep %.2f ms (dedupe %.2f, structure %.2f), pick-to-copy %.2f "
+              "ms, %zu B in\n",
+              n, tl_merge_ms, ms_since(t_prep0), t_dedupe_ms, t_struct_ms, ms_since(tl_run_t0), in_bytes);
     // The input copy goes on the run's signature stream, or (copy_stream, when none of the run's buffers was
     // reallocated in that stream's order) on the device's table stream: a previous run's tail still queued on the
     // signature stream of this pair then delays only this run's signature branch, not its message branch
@@ -1506,46 +1543,76 @@ void run_merged(Device& d, Slot& sl, const std::vector<Task>& parts, std::vector
       if (b.set_pk_first) npk += b.set_pk_first[sh.set_end] - b.set_pk_first[sh.set_begin];
       max_index = std::max(max_index, t.call->max_index);
     }
-    std::vector<uint32_t> jfs{0}, siglen, spf{0}, pki;
-    std::vector<uint8_t> flags, pkb, msgs, sigs;
+    // the parts' offsets (sets, jobs, pubkeys), then every part packed in parallel into its own ranges: the batch
+    // scalars (ChaCha20, ~0.4 ms per 16k-set call) and the copies of a 131k-set run took ~2.5 ms on one thread
+    uint32_t sig_w = 96;
+    std::vector<uint32_t> p_so, p_jo, p_ko;
+    {
+      uint32_t so = 0, jo = 0, ko = 0;
+      for (size_t p : live) {
+        const Task& t = parts[p];
+        const Shard& sh = t.call->shards[t.shard];
+        const blsgpu_batch& b = t.call->b;
+        p_so.push_back(so);
+        p_jo.push_back(jo);
+        p_ko.push_back(ko);
+        so += sh.set_end - sh.set_begin;
+        jo += sh.job_end - sh.job_begin;
+        if (b.set_pk_first) ko += b.set_pk_first[sh.set_end] - b.set_pk_first[sh.set_begin];
+        for (uint32_t i = sh.set_begin; i < sh.set_end && sig_w == 96; i++)
+          if (b.sig_len[i] == 192) sig_w = 192;
+      }
+    }
+    std::vector<uint32_t> jfs(nj + 1), siglen(n), spf(mode == 1 ? 1 : n + 1), pki(mode == 0 ? npk : 0);
+    std::vector<uint8_t> flags(nj), pkb(mode == 1 ? (size_t)n * 96 : mode == 2 ? (size_t)npk * 96 : 0),
+        msgs((size_t)n * 32), sigs((size_t)n * sig_w, 0);
     std::vector<uint64_t> scal(std::max<uint32_t>(n, 1));
-    jfs.reserve(nj + 1);
-    siglen.reserve(n);
-    msgs.reserve((size_t)n * 32);
-    sigs.reserve((size_t)n * 192);
-    if (mode == 0) pki.reserve(npk);
-    if (mode == 1) pkb.reserve((size_t)n * 96);
-    if (mode == 2) pkb.reserve((size_t)npk * 96);
-    uint32_t so = 0;
-    for (size_t p : live) {
-      const Task& t = parts[p];
+    jfs[0] = 0;
+    spf[0] = 0;
+    auto pack = [&](size_t q) {
+      const Task& t = parts[live[q]];
       const Shard& sh = t.call->shards[t.shard];
       const blsgpu_batch& b = t.call->b;
+      const uint32_t so = p_so[q], jo = p_jo[q], ko = p_ko[q], ns = sh.set_end - sh.set_begin;
       shard_scalars(b, sh, t.call->key, scal.data() + so);
       for (uint32_t j = sh.job_begin; j < sh.job_end; j++) {
-        jfs.push_back(so + b.job_first_set[j + 1] - sh.set_begin);
-        flags.push_back(b.job_flags ? b.job_flags[j] : 0);
+        jfs[jo + (j - sh.job_begin) + 1] = so + b.job_first_set[j + 1] - sh.set_begin;
+        flags[jo + (j - sh.job_begin)] = b.job_flags ? b.job_flags[j] : 0;
       }
-      for (uint32_t i = sh.set_begin; i < sh.set_end; i++) {
-        const uint32_t len = b.sig_len[i];
-        siglen.push_back(len);
-        const size_t at = sigs.size();
-        sigs.resize(at + 192, 0);
-        if (len == 96 || len == 192) memcpy(sigs.data() + at, b.sigs + (size_t)i * b.sig_stride, len);
-      }
-      msgs.insert(msgs.end(), b.msgs + (size_t)sh.set_begin * 32, b.msgs + (size_t)sh.set_end * 32);
-      if (mode == 1) {
-        pkb.insert(pkb.end(), b.pk_bytes + (size_t)sh.set_begin * 96, b.pk_bytes + (size_t)sh.set_end * 96);
+      memcpy(siglen.data() + so, b.sig_len + sh.set_begin, (size_t)ns * 4);
+      if (b.sig_stride == sig_w) {
+        memcpy(sigs.data() + (size_t)so * sig_w, b.sigs + (size_t)sh.set_begin * sig_w, (size_t)ns * sig_w);
       } else {
-        const uint32_t k0 = b.set_pk_first[sh.set_begin];
-        for (uint32_t i = sh.set_begin; i < sh.set_end; i++)
-          spf.push_back(spf.back() + b.set_pk_first[i + 1] - b.set_pk_first[i]);
-        if (mode == 0)
-          pki.insert(pki.end(), b.pk_index + k0, b.pk_index + b.set_pk_first[sh.set_end]);
-        else
-          pkb.insert(pkb.end(), b.pk_bytes + (size_t)k0 * 96, b.pk_bytes + (size_t)b.set_pk_first[sh.set_end] * 96);
+        for (uint32_t i = sh.set_begin; i < sh.set_end; i++) {
+          const uint32_t len = b.sig_len[i];
+          if (len == 96 || len == 192)
+            memcpy(sigs.data() + (size_t)(so + i - sh.set_begin) * sig_w, b.sigs + (size_t)i * b.sig_stride, len);
+        }
       }
-      so += sh.set_end - sh.set_begin;
+      memcpy(msgs.data() + (size_t)so * 32, b.msgs + (size_t)sh.set_begin * 32, (size_t)ns * 32);
+      if (mode == 1) {
+        memcpy(pkb.data() + (size_t)so * 96, b.pk_bytes + (size_t)sh.set_begin * 96, (size_t)ns * 96);
+      } else {
+        const uint32_t k0 = b.set_pk_first[sh.set_begin], k1 = b.set_pk_first[sh.set_end];
+        for (uint32_t i = sh.set_begin; i < sh.set_end; i++)
+          spf[so + (i - sh.set_begin) + 1] = ko + b.set_pk_first[i + 1] - k0;
+        if (mode == 0)
+          memcpy(pki.data() + ko, b.pk_index + k0, (size_t)(k1 - k0) * 4);
+        else
+          memcpy(pkb.data() + (size_t)ko * 96, b.pk_bytes + (size_t)k0 * 96, (size_t)(k1 - k0) * 96);
+      }
+    };
+    {  // parts of >= 4,096 sets on their own threads (a small part packs faster than a thread starts)
+      std::vector<std::thread> th;
+      for (size_t q = 1; q < live.size(); q++) {
+        const Shard& sh = parts[live[q]].call->shards[parts[live[q]].shard];
+        if (sh.set_end - sh.set_begin >= 4096) th.emplace_back(pack, q);
+      }
+      for (size_t q = 0; q < live.size(); q++) {
+        const Shard& sh = parts[live[q]].call->shards[parts[live[q]].shard];
+        if (q == 0 || sh.set_end - sh.set_begin < 4096) pack(q);
+      }
+      for (auto& x : th) x.join();
     }
     blsgpu_batch mb{};
     mb.n_sets = n;
@@ -1558,7 +1625,7 @@ void run_merged(Device& d, Slot& sl, const std::vector<Task>& parts, std::vector
     mb.msgs = msgs.data();
     mb.sigs = sigs.data();
     mb.sig_len = siglen.data();
-    mb.sig_stride = 192;
+    mb.sig_stride = sig_w;
     res.assign(std::max<uint32_t>(nj, 1), 0);
     const Shard all{0, nj, 0, n};
     tl_merge_ms = ms_since(t_merge0);
