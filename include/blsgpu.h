@@ -257,6 +257,11 @@ const char* blsgpu_code_name(int code);
  *       the batch scalar r = a + b*lambda of a scalar word w (a = 2 lo + 1 - 2^32, b = 2 hi + 1 - 2^32 from w's
  *       32-bit halves, lambda = -z^2), word 0 = r = 1
  *     11 fp_lc(raw limbs: 15 x 14 LE words -> 14 words): the lazily reduced combination x0 + .. + x6 - x7 - .. - x14
+ *     16 final_exp / 17 miller (the cooperative GT engine, 576 / 288 -> 576)
+ *     18 lane-pair G2 arithmetic (fp2x.hpp) against the one-lane forms: P, Q affine (384) -> [|z|]P affine (192);
+ *        status = bitmask of the cases (add, add doubling / infinity branches, dbl, mixed add, psi, psi^2, [|z|],
+ *        Fp2 product / square) where the lane-pair result differs
+ * Strides below an op's element size, and unknown ops, are refused with BLSGPU_ERR_ARGS.
  * Returns BLSGPU_OK or an error. */
 int blsgpu_debug_op(blsgpu_ctx* ctx, int op, uint32_t n, const uint8_t* in, uint32_t in_stride,
                     uint8_t* out, uint32_t out_stride, int32_t* status);

@@ -182,6 +182,79 @@ __global__ __launch_bounds__(GTW_MILLER_LANES) void k_debug_gt(int op, const uin
   }
 }
 
+// Lane-pair G2 arithmetic against the one-lane forms (op 18; fp2x.hpp), lane pair per element: input P, Q affine
+// (192 B each).  The pair builds P, Q in Jacobian form with Z != 1 (P scaled by l = 2 + i, Q by l + 1), computes
+// P + Q, P + P (the addition's doubling branch), P + (-P) (its infinity branch), P + O, O + Q, 2P, P + Q_affine,
+// psi(P), psi^2(P), [|z|]P and the Fp2 product / square of P.x, Q.y; lane 0 gathers each result and compares it with
+// the same operation on one lane (jac_eq, or Fp2 equality).  status = bit k set when case k differs; out = [|z|]P
+// affine (192 B) from the pair's result, for an oracle check.
+__global__ __launch_bounds__(WAVE) void k_debug_pairs(uint32_t n, const uint8_t* in, uint32_t in_stride, uint8_t* out,
+                                                      uint32_t out_stride, int32_t* status) {
+  const uint32_t q = blockIdx.x * WAVE + threadIdx.x, i = q >> 1, k = q & 1;
+  if (i >= n) return;
+  const uint8_t* a = in + (size_t)i * in_stride;
+  const g2a Pa = dbg_load_g2(a), Qa = dbg_load_g2(a + 192);
+  fp l1 = fp_zero();
+  l1.l[0] = 2 + i;
+  l1 = fp_to_mont(l1);
+  const fp2 lp = fp2_make(l1, FP_ONE), lq = fp2_make(fp_add(l1, FP_ONE), FP_ONE);
+  auto scale = [](const g2a& p, const fp2& l) {
+    g2j r;
+    const fp2 l2 = fp2_sqr(l);
+    r.x = fp2_mul(p.x, l2);
+    r.y = fp2_mul(p.y, fp2_mul(l2, l));
+    r.z = l;
+    return r;
+  };
+  const g2j P = scale(Pa, lp), Q = scale(Qa, lq), O = jac_infinity<fp2>();
+  auto x_of = [&](const g2j& v) {
+    g2jx r;
+    r.x = fp2x_of(v.x);
+    r.y = fp2x_of(v.y);
+    r.z = fp2x_of(v.z);
+    return r;
+  };
+  auto gather = [&](const g2jx& v) {  // both lanes: the full point
+    g2j r;
+    const fp ox = fp_swap(v.x.v), oy = fp_swap(v.y.v), oz = fp_swap(v.z.v);
+    r.x = k ? fp2_make(ox, v.x.v) : fp2_make(v.x.v, ox);
+    r.y = k ? fp2_make(oy, v.y.v) : fp2_make(v.y.v, oy);
+    r.z = k ? fp2_make(oz, v.z.v) : fp2_make(v.z.v, oz);
+    return r;
+  };
+  auto gather2 = [&](const fp2x& v) {
+    const fp o2 = fp_swap(v.v);
+    return k ? fp2_make(o2, v.v) : fp2_make(v.v, o2);
+  };
+  const g2jx Px = x_of(P), Qx = x_of(Q), Ox = x_of(O);
+  aff<fp2x> Qax;
+  Qax.x = fp2x_of(Qa.x);
+  Qax.y = fp2x_of(Qa.y);
+  const g2j r0 = gather(jac_add(Px, Qx)), r1 = gather(jac_add(Px, Px)), r2 = gather(jac_add(Px, jac_neg(Px))),
+            r3 = gather(jac_add(Px, Ox)), r4 = gather(jac_add(Ox, Qx)), r5 = gather(jac_dbl(Px)),
+            r6 = gather(jac_add_aff(Px, Qax)), r7 = gather(g2_psi(Px)), r8 = gather(g2_psi2(Px)),
+            r9 = gather(jac_mul_zabs(Px));
+  const fp2 m0 = gather2(F_mul(Px.x, Qx.y)), m1 = gather2(F_sqr(Px.x));
+  if (k == 0) {
+    int st = 0;
+    st |= jac_eq(r0, jac_add(P, Q)) ? 0 : 1;
+    st |= jac_eq(r1, jac_dbl(P)) ? 0 : 2;
+    st |= jac_is_inf(r2) ? 0 : 4;
+    st |= jac_eq(r3, P) ? 0 : 8;
+    st |= jac_eq(r4, Q) ? 0 : 16;
+    st |= jac_eq(r5, jac_dbl(P)) ? 0 : 32;
+    st |= jac_eq(r6, jac_add_aff(P, Qa)) ? 0 : 64;
+    st |= jac_eq(r7, g2_psi(P)) ? 0 : 128;
+    st |= jac_eq(r8, g2_psi2(P)) ? 0 : 256;
+    st |= jac_eq(r9, jac_mul_zabs(P)) ? 0 : 512;
+    st |= fp2_eq(m0, fp2_mul(P.x, Q.y)) ? 0 : 1024;
+    st |= fp2_eq(m1, fp2_sqr(P.x)) ? 0 : 2048;
+    g2a z;
+    if (jac_to_aff(r9, z)) g2a_to_be192(z, out + (size_t)i * out_stride);
+    status[i] = st;
+  }
+}
+
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
 void launch_debug_op(int op, uint32_t n, const uint8_t* in, uint32_t in_stride, uint8_t* out, uint32_t out_stride,
@@ -189,6 +262,8 @@ void launch_debug_op(int op, uint32_t n, const uint8_t* in, uint32_t in_stride, 
   if (!n) return;
   if (op == 16 || op == 17)
     hipLaunchKernelGGL(k_debug_gt, dim3(n), dim3(GTW_MILLER_LANES), 0, s, op, in, in_stride, out, out_stride, status);
+  else if (op == 18)
+    hipLaunchKernelGGL(k_debug_pairs, grid_for(2 * n), dim3(WAVE), 0, s, n, in, in_stride, out, out_stride, status);
   else
     hipLaunchKernelGGL(k_debug_op, grid_for(n), dim3(WAVE), 0, s, op, n, in, in_stride, out, out_stride, status);
 }

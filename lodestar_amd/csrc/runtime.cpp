@@ -153,7 +153,7 @@ struct Task {
 
 // The device's pipeline streams, shared by its slots: one per branch of a run's DAG (run_shard).  Runs of different
 // slots queue behind each other per branch, so the chip always has the next run's work while one run's tail drains.
-enum { kSig = 0, kMsg = 1, kPk = 2, kTail = 3, kStreams = 4 };
+enum { kSig = 0, kMsg = 1, kPk = 2, kTail = 3, kStreams = 4, kMaxPairs = 3 };
 // streams created with the device's highest priority (bit k = stream k); see blsgpu_init
 #ifndef BLSGPU_STREAM_PRIO
 #define BLSGPU_STREAM_PRIO ((1 << kMsg) | (1 << kTail))
@@ -170,7 +170,8 @@ enum { kSig = 0, kMsg = 1, kPk = 2, kTail = 3, kStreams = 4 };
 struct Device {
   int id = 0;
   hipStream_t table_stream = nullptr;  // uploads and the synchronous helpers (debug, aggregate, ...)
-  hipStream_t st[kStreams] = {};
+  hipStream_t st[2 * kMaxPairs] = {};
+  int npairs = 2;  // stream pairs in use: 3 when the process has >= 6 hardware queues (a pair per slot)
   std::mutex enq_mu;  // one run's batch (or fallback) launches are enqueued without another slot's in between
   std::mutex helper_mu;
   Slot helper;  // buffers of the synchronous helpers (on table_stream)
@@ -743,7 +744,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   else
     in_bytes = o_pk + (size_t)n * 96;
   const size_t o_pk2 = al256(o_pk + (size_t)(n + 1) * 4);
-  const int par = BLSGPU_STREAM_PAIRS ? (int)(d.run_seq.fetch_add(1) & 1u) : 0;
+  const int par = BLSGPU_STREAM_PAIRS ? (int)(d.run_seq.fetch_add(1) % (uint32_t)d.npairs) : 0;
+  const int other = (par + 1) % d.npairs;
   hipStream_t s = BLSGPU_STREAM_PAIRS ? d.st[2 * par] : d.st[kSig];
   sl.set_stream(s);  // buffer growth of the batch pass, ordered before the input copy on the same stream
   sl.h_in.ensure(in_bytes);
@@ -893,7 +895,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // its own signature decode and subgroup checks instead of in front of them: the signature branch was a small
   // call's critical path (C1 serial trace: 7.25 ms vs the message branch's 6.15).
   hipStream_t sm = BLSGPU_STREAM_PAIRS ? d.st[2 * par + 1] : d.st[kMsg],
-              sp = BLSGPU_STREAM_PAIRS ? (small && sl.alone ? d.st[2 * (1 - par)] : s) : d.st[kPk],
+              sp = BLSGPU_STREAM_PAIRS ? (small && sl.alone ? d.st[2 * other] : s) : d.st[kPk],
               stl = BLSGPU_STREAM_PAIRS ? s : d.st[kTail];
   if (opt.serial) sm = sp = stl = s;
   auto beg = [&](int k, hipStream_t st) {
@@ -951,7 +953,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     // enters, and a dropped valid signature is in G2, so its term e(-g1, r sig) != 1) and its jobs are re-checked one
     // by one with exact masks (the fallback), while a clean group's S is exact.  Saves the MSM's ~1.5 ms on the
     // signature branch of a 128-set call.
-    hipStream_t smsm = spec ? d.st[2 * (1 - par) + 1] : s;
+    hipStream_t smsm = spec ? d.st[2 * other + 1] : s;
     PipelineBuffers pbm = pb;
     if (spec) pbm.include = db + ob_spec;
     beg(0, s);
@@ -1998,8 +2000,11 @@ int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
       // priorities, 2.94M message stream, 2.945M message + tail; profiles/r03_ab6_stream_priority.txt.)
       int prio_lo = 0, prio_hi = 0;
       HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-      for (int k = 0; k < kStreams; k++) {
-        const bool high = (BLSGPU_STREAM_PRIO & (1 << k)) != 0;
+      // a third stream pair when the process has the hardware queues for it (GPU_MAX_HW_QUEUES >= 6): each of the
+      // default three slots' runs then has its own pair, and a run never queues behind another run's tail
+      d->npairs = ctx->hw_queues >= 6 ? kMaxPairs : 2;
+      for (int k = 0; k < 2 * d->npairs; k++) {
+        const bool high = (BLSGPU_STREAM_PRIO & (1 << (k & 3))) != 0 || (k >= kStreams && (k & 1));
         HIPCHK(hipStreamCreateWithPriority(&d->st[k], hipStreamNonBlocking, high ? prio_hi : prio_lo));
       }
     }
@@ -2590,6 +2595,19 @@ int blsgpu_signing_roots(blsgpu_ctx* ctx, int kind, uint32_t n, const uint8_t* o
 int blsgpu_debug_op(blsgpu_ctx* ctx, int op, uint32_t n, const uint8_t* in, uint32_t in_stride, uint8_t* out,
                     uint32_t out_stride, int32_t* status) {
   if (!ctx || ctx->devs.empty() || !in || !out || !status) return BLSGPU_ERR_ARGS;
+  // the bytes each op reads per element and writes per element (k_debug.hip): a smaller stride is refused here, so a
+  // test hook can never read or write past its buffers on the device
+  struct OpSize {
+    int op;
+    uint32_t in, out;
+  };
+  static const OpSize kOpSizes[] = {{0, 96, 48},    {1, 194, 192},  {2, 32, 192},   {3, 288, 576},  {4, 576, 576},
+                                    {5, 104, 96},   {6, 200, 192},  {7, 64, 96},    {8, 32, 96},    {9, 200, 2880},
+                                    {10, 104, 1440}, {11, 840, 56}, {16, 576, 576}, {17, 288, 576}, {18, 384, 192}};
+  const OpSize* sz = nullptr;
+  for (const OpSize& o : kOpSizes)
+    if (o.op == op) sz = &o;
+  if (!sz || in_stride < sz->in || out_stride < sz->out) return BLSGPU_ERR_ARGS;
   if (n == 0) return BLSGPU_OK;
   if (!enter(ctx)) return BLSGPU_ERR_CLOSED;
   Device* d = ctx->devs[0];

@@ -90,9 +90,13 @@ STAGES = ["sig_decode", "hash_to_g2", "pk_aggregate", "pk_finish", "sig_msm", "m
           "group_reduce", "group_check"]
 # the kernels each stage's HIP-event interval covers (rocprof lists them separately; k_batch_inv runs in both the
 # hash and the pubkey stage)
-KERNEL_OF_STAGE = ["k_sig_decode", "k_hash_prep+k_batch_inv+k_hash_map+k_hash_clear+k_hash_clear_coop+k_h_affine", "k_pk_aggregate",
-                   "k_pk_finish+k_batch_inv+k_pk_affine", "k_job_mask+k_msm_bucket+k_msm_window+k_msm_horner",
-                   "k_miller_lines+k_miller_acc", "k_f_runs+k_f_pairs+k_f_gather", "k_group_sig_miller+k_group_check"]
+KERNEL_OF_STAGE = ["k_sig_decode+k_sig_subgroup2+k_sig_subgroup_coop",
+                   "k_hash_prep+k_batch_inv+k_hash_map+k_hash_clear+k_hash_clear2+k_hash_clear_coop+k_h_affine",
+                   "k_pk_aggregate+k_pk_aggregate_g", "k_pk_finish+k_batch_inv+k_pk_affine",
+                   "k_job_mask+k_msm_bucket+k_msm_bucket2+k_msm_slice_pairs+k_msm_slice_pairs2+k_msm_window+k_msm_window2"
+                   "+k_msm_horner+k_msm_horner_lane",
+                   "k_miller_lines+k_miller_lines2+k_miller_acc+k_miller_acc2+k_miller_acc6+k_miller_accx+k_miller_coop",
+                   "k_f_runs+k_f_pairs+k_f_gather", "k_group_sig_miller+k_group_check"]
 
 
 DONE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)

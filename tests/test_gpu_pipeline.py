@@ -274,3 +274,24 @@ def test_fp_lc_device_edges(ctx):
         v = sum(int(x) << (28 * i) for i, x in enumerate(r))
         assert (r[:13] < (1 << 28)).all() and v < 1.003 * P
         assert v % P == (sum(xs[:7]) - sum(xs[7:])) % P
+
+
+def test_lane_pair_g2_arithmetic_vs_one_lane(ctx):
+    """The lane-pair G2 formulas (fp2x.hpp: hash_clear2, sig_subgroup2, msm_bucket2, miller_lines2) against the one-lane
+    forms on the same points, including the addition's exceptional branches (P + P, P + (-P), infinity operands) and
+    Jacobian inputs with Z != 1 (debug op 18), over the reference-held mainnet G2 corpus; [|z|]P also against the
+    oracle."""
+    import json
+    import os
+
+    pts = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "mainnet_g2_points.json")))["points"]
+    aff = [bls.signature_from_bytes(bytes.fromhex(h), validate=False) for h in pts]
+    n = len(aff)
+    inp = b"".join(g2b(aff[i]) + g2b(aff[(i + 1) % n]) for i in range(n))
+    out, st = ctx.debug_op(18, inp, 384, 192)
+    assert (st == 0).all(), st
+    for i in range(n):  # [|z|]P by the oracle
+        want = bls.g2_mul(aff[i], bls.BLS_X_ABS)
+        assert out[192 * i: 192 * i + 192] == g2b(want)
+    with pytest.raises(RuntimeError, match="ERR_ARGS"):
+        ctx.debug_op(18, inp, 383, 192)  # a stride below the op's element is refused on the host
