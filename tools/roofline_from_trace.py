@@ -41,8 +41,11 @@ def main(trace, bench_json, out=None):
         c["end"] = max(c["end"], e)
         c["kernel_ns"] += e - s
         c["kernels"] += 1
-    # only runs whose last kernel (names[-1]) landed inside the window
-    done = [r for r in runs if r["kernels"] >= len(names)]
+        if n == names[-1]:
+            c["complete"] = True
+    # only runs whose last kernel (names[-1]) landed inside the window (the stage lists alternative forms, e.g. the
+    # lane-pair and cooperative clearings, so a run launches fewer kernels than the list names)
+    done = [r for r in runs if r.get("complete")]
     span = sum(r["end"] - r["start"] for r in done) / len(done) / 1e6
     busy = sum(r["kernel_ns"] for r in done) / len(done) / 1e6
     prods = rf["algorithmic_products_per_launch"] * rf["launches_timed"] / max(len(done), 1)

@@ -61,11 +61,14 @@ def main(path, out):
                      "dispatches",
            "weighted_frac_active_valu": round(sum(v["frac_active_valu"] * v["wave_cycles"] for v in path_k.values())
                                               / tot_wc, 4),
-           "note": "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: the fraction of a resident wave's cycles spent issuing VALU. "
-                   "The stage kernels hold one 512-register wave per SIMD, and one wave alone issues a plain VALU "
-                   "instruction every ~4 cycles and a v_mad_u64_u32 every ~10 (profiles/r02_mad_chain.json) -- half "
-                   "the SIMD's rate with two waves -- so ~0.75 VALU-active is close to the one-wave issue ceiling; "
-                   "the remaining lever at one wave is fewer instructions per product.",
+           "note": "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: the fraction of a resident wave's cycles spent issuing VALU "
+                   "(per wave, not per SIMD). The one-lane stage kernels hold one 512-register wave per SIMD, so theirs "
+                   "is the SIMD's; the lane-pair and two-wave kernels (k_hash_clear2, k_sig_subgroup2, k_hash_map, "
+                   "k_sig_decode, k_msm_bucket2, k_miller_lines2) share a SIMD with a second "
+                   "wave, so a wave waits while its partner issues (counted in SQ_WAIT_INST_ANY) and the SIMD's VALU "
+                   "share is up to twice the per-wave figure. One wave alone issues a plain VALU instruction every ~4 "
+                   "cycles and a v_mad_u64_u32 every ~10 (profiles/r02_mad_chain.json) -- half the SIMD's rate with "
+                   "two waves.",
            "kernels": dict(sorted(kernels.items(), key=lambda kv: -kv[1]["wave_cycles"]))}
     with open(out, "w") as fh:
         json.dump(doc, fh, indent=1)
