@@ -168,7 +168,7 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * of 1k-32k sets, 8..256, default 32), "msm_tree" (those runs sum each range's slices by a pairwise tree, 0/1,
  * default 1), "f_run_max" (merged runs: longest lane-serial run of the F product tree, a power of two, default 16),
  * "coop_max" / "coop_g2_max" (runs of <= this many pairings / sets take the cooperative Miller loops / [|z|] chains,
- * default 384 / 4096), "coop_excl_max" (cooperative workgroups take a CU each in runs of <= this many items, default
+ * default 512 / 4096), "coop_excl_max" (cooperative workgroups take a CU each in runs of <= this many items, default
  * 512), "rsig_spec" (small idle runs form every r_i sig_i beside the batch pass for a possible fallback, 0/1, default
  * 1), "fb_lane_min" (fallback check launches of >= this many checks in large runs take one lane per check, default
  * 256, 0 = never), "route_split_sets" (see blsgpu_route_call, default 16384), "acc6_max" (runs of one-item Miller chunks up to this many

@@ -221,7 +221,7 @@ struct Options {  // snapshot taken at the start of each call
   int64_t tail_on_msg = 0;        // the group stage runs on the pair's high-priority message stream
   int64_t copy_stream = 0;        // a run's input copy on the table stream (not behind the pair's previous tail)
   int64_t msm_tree = 1;           // those runs sum each range's slices by a pairwise tree
-  int64_t coop_max = 384;         // runs of <= this many pairings take the cooperative Miller loops (k_miller_coop)
+  int64_t coop_max = 512;         // runs of <= this many pairings take the cooperative Miller loops (k_miller_coop)
   int64_t coop_g2_max = 4096;     // runs of <= this many sets take the cooperative [|z|] chains (clearing, subgroup)
   int64_t coop_excl_max = 512;    // cooperative workgroups take a CU each only in runs of <= this many items
   int64_t rsig_spec = 1;          // small idle runs form every r_i sig_i beside the batch pass (for the fallback)

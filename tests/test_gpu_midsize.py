@@ -69,11 +69,11 @@ def compare(ctx, call, seed=bench.SEED):
     return got, st
 
 
-@pytest.mark.parametrize("n", [1024, 2048, 4096, 8192])
+@pytest.mark.parametrize("n", [512, 513, 1024, 2048, 4096, 8192])
 def test_midsize_one_percent_corrupt_vs_oracle(ctx, pool, n):
-    """The verdict's mid-size parity: 1k / 2k / 4k / 8k sets, ~1% corrupted, at the runtime defaults (1k and 2k take
-    the cooperative Miller loops, up to 4k the cooperative chains, 8k the lane forms); the failed groups' per-job
-    checks reuse the batch pass's Miller values."""
+    """The verdict's mid-size parity: 1k / 2k / 4k / 8k sets, ~1% corrupted, at the runtime defaults (up to 512
+    pairings the cooperative Miller loops -- 512 / 513 sit on either side of that edge --, up to 4k the cooperative
+    chains, 8k the lane forms); the failed groups' per-job checks reuse the batch pass's Miller values."""
     call, applied = make_call(pool, n, 0x5000 + n)
     assert len(applied) >= n // 200
     got, st = compare(ctx, call)
