@@ -225,6 +225,7 @@ struct Options {  // snapshot taken at the start of each call
   int64_t coop_g2_max = 4096;     // runs of <= this many sets take the cooperative [|z|] chains (clearing, subgroup)
   int64_t coop_excl_max = 512;    // cooperative workgroups take a CU each only in runs of <= this many items
   int64_t rsig_spec = 1;          // small idle runs form every r_i sig_i beside the batch pass (for the fallback)
+  int64_t spec_large = 1;         // runs above small_max on an idle device take the speculative MSM too
   int64_t fb_lane_min = 256;      // fallback check launches of >= this many checks take one lane per check (0 = never)
   int64_t route_split_sets = 16384;  // a call is split over min(devices, sets / this) devices, else routed whole
   int64_t acc6_max = 16384;       // one-item-chunk runs of <= this many chunks take the six-lane accumulation
@@ -241,7 +242,7 @@ struct Options {  // snapshot taken at the start of each call
            lane_tail_parts == o.lane_tail_parts &&
            msm_slice_mid == o.msm_slice_mid && msm_tree == o.msm_tree &&
            lines_lanes == o.lines_lanes && merge_balance == o.merge_balance && early_release == o.early_release && tail_on_msg == o.tail_on_msg && copy_stream == o.copy_stream && coop_max == o.coop_max &&
-           coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec &&
+           coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec && spec_large == o.spec_large &&
            fb_lane_min == o.fb_lane_min && acc6_max == o.acc6_max && miller_pairs == o.miller_pairs && small_max == o.small_max &&
            fb_direct_min == o.fb_direct_min && fb_check6 == o.fb_check6 && fb_force_busy == o.fb_force_busy;
   }
@@ -651,11 +652,12 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // the other stream pair too (speculative MSM, parallel pubkey branch, r_i sig_i), and its fallback checks stay
   // cooperative (latency) instead of lane-per-check (throughput).
   const bool small = n <= (uint32_t)opt.small_max;
-  const bool spec = BLSGPU_STREAM_PAIRS && small && sl.alone && !opt.serial;  // speculative MSM (kernel pipeline below)
+  // speculative MSM (kernel pipeline below); spec_large: larger runs on an idle device too
+  const bool spec = BLSGPU_STREAM_PAIRS && (small || opt.spec_large) && sl.alone && !opt.serial;
   // A small run on an idle device also forms every r_i sig_i (k_sig_scale) on the idle pubkey stream once its pubkeys
   // and the decode are done: the chip has room, and a failed group's per-job checks then start from the sums instead
   // of a 1.7 ms scaling launch on the fallback's critical path (the batch pass itself never reads them).
-  const bool rsig_spec = spec && opt.rsig_spec;
+  const bool rsig_spec = spec && small && opt.rsig_spec;
   // MSM slices of the groups' set ranges (S_g = sum r_i sig_i).  Runs up to 32k sets (an isolated block's or
   // gossip call's latency) take half slices: twice the bucket workgroups at half the chain, 16k isolated sig_msm
   // 3.55 -> 2.80 ms; merged runs keep full slices (fewer bucket sums to combine: 100-step C2 3.13M vs 3.01M).
@@ -2189,6 +2191,8 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
     ctx->opt.coop_excl_max = value;
   } else if (k == "rsig_spec") {
     ctx->opt.rsig_spec = value != 0;
+  } else if (k == "spec_large") {
+    ctx->opt.spec_large = value != 0;
   } else if (k == "fb_lane_min") {
     if (value < 0) return BLSGPU_ERR_ARGS;
     ctx->opt.fb_lane_min = value;
@@ -2277,6 +2281,7 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "coop_g2_max") *value = o.coop_g2_max;
   else if (k == "coop_excl_max") *value = o.coop_excl_max;
   else if (k == "rsig_spec") *value = o.rsig_spec;
+  else if (k == "spec_large") *value = o.spec_large;
   else if (k == "fb_lane_min") *value = o.fb_lane_min;
   else if (k == "route_split_sets") *value = o.route_split_sets;
   else if (k == "acc6_max") *value = o.acc6_max;

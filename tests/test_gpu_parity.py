@@ -138,6 +138,29 @@ def test_full_size_single_sets_vs_oracle(ctx, n, tag):
     assert (res == 1).all() and st.batch_retries == 0
 
 
+def test_speculative_msm_large_idle_run_vs_oracle(ctx):
+    """spec_large: a 16,384-set call on an idle device takes the speculative MSM (over the sets that decoded, on the
+    other pair's message stream) -- the corrupted sets' groups must still come out job for job as the oracle's (their
+    clean jobs re-checked with exact masks), and a clean call must pass without retries."""
+    n, tag = 16384, b"SP"
+    rng = np.random.default_rng(7)
+    sks, pks, msgs, sigs, sig_len = corrupted_single_sets(n, tag, rng)
+    base = dict(sigs=sigs, sig_len=sig_len, msgs=b"".join(msgs), sig_stride=192)
+    old = ctx.get_option("spec_large")
+    ctx.set_option("spec_large", 1)
+    try:
+        got, st = compare(ctx, job_first_set=np.arange(n + 1), pk_bytes=pks, job_flags=np.ones(n), **base)
+        assert (got < 0).sum() >= 4 and st.batch_retries >= 1
+        jfs = np.arange(0, n + 1, 128)
+        compare(ctx, job_first_set=jfs, pk_bytes=pks, job_flags=np.ones(len(jfs) - 1), **base)
+        good = cpu.sign(sks, b"".join(msg(j, tag) for j in range(n)), threads=THREADS)
+        res, st = ctx.verify_raw(np.arange(n + 1), good, [96] * n, b"".join(msg(j, tag) for j in range(n)),
+                                 pk_bytes=pks, job_flags=np.ones(n))
+        assert (res == 1).all() and st.batch_retries == 0
+    finally:
+        ctx.set_option("spec_large", old)
+
+
 def test_device_signing_matches_oracle(ctx):
     """The bench generates its workload with the device's sign / sk_to_pk ops: pin them to the oracle."""
     n = 256
