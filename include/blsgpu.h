@@ -175,7 +175,14 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * 256, 0 = never), "route_split_sets" (see blsgpu_route_call, default 16384), "acc6_max" (runs of one-item Miller chunks up to this many
  * take the six-lane accumulation, default 16384; "miller_lanes" 6 forces it), "miller_pairs" (larger runs take the
  * lane-pair accumulation, every Fp2 split over two lanes at two waves per SIMD, 0/1, default 0; "miller_lanes" 3
- * forces it for every run),
+ * forces it for every run), "small_max" (runs of <= this many sets are latency-first: on an idle device the
+ * parallel pubkey branch and r_i sig_i, cooperative fallback checks; default 4096), "fb_direct_min" (large runs under
+ * load with >= this many retried jobs check each one directly, default 1024, 0 = never), "fb_check6" (those checks: 0
+ * one lane each, 1 Miller loop on one lane and the final exponentiation on six, 2 both on six lanes; default 2),
+ * "fb_force_busy" (tests: every run's fallback takes the under-load forms, 0/1, default 0), "early_release" /
+ * "tail_on_msg" / "copy_stream" (run-formation experiments, 0/1, default 0: a run leaves the pipeline count when its
+ * message branch is done / the group stage on the pair's high-priority message stream / the input copy on the table
+ * stream),
  * "lane_tail_min" / "lane_tail_parts" (runs of >= lane_tail_min sets take lane forms of the Horner passes (bit 0)
  * and of MillerLoop(-g1, S) (bit 1) instead of the cooperative workgroups; default 0 = never, parts 3), "serial"
  * (diagnostics: every branch of a run on one stream, so each kernel runs alone on the chip; 0/1, default 0), "profile" (per-stage kernel times in
