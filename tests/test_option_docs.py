@@ -24,3 +24,12 @@ def test_every_option_documented():
     assert sorted(k for k in set_keys if f"`{k}`" not in integration) == []
     assert get_keys - set_keys == {"hw_queues", "abi_version"}
     assert set_keys <= get_keys
+
+
+def test_gpu_option_test_covers_every_key():
+    """tests/test_gpu_options.py round-trips every key but "slots" (resizing the dispatcher pool has its own tests)."""
+    set_keys, _ = _keys()
+    gpu_test = open(os.path.join(ROOT, "tests", "test_gpu_options.py")).read()
+    covered = set(re.findall(r'"([a-z0-9_]+)": \(', gpu_test))
+    assert sorted(set_keys - covered) == ["slots"]
+    assert covered <= set_keys
