@@ -423,6 +423,55 @@ def cpu_baseline(call, expected, table, hc):
 
 
 PARITY_SEED = SEED + 0x5041524954  # "PARIT"
+URGENT_SEED = SEED + 0x55524745  # "URGE"
+
+
+def urgent_calls(ctx, work, n_calls=32):
+    """Latency-critical calls (the reference's verifyOnMainThread: the gossip block proposer signature, one set, and
+    verifySignatureSet users; chain/validation/block.ts:146, multithread/index.ts:138-151): n_calls calls alternating 1
+    and 3 single-pubkey sets, each one job flagged BLSGPU_JOB_URGENT (not batchable), keys from the step's device table,
+    fresh signing roots signed on the GPU before timing.  Returns [(sets, call kwargs)]."""
+    from lodestar_amd.native import JOB_URGENT
+
+    out = []
+    sks, k = work["_sk"], 0
+    for c in range(n_calls):
+        n = 1 if c % 2 == 0 else 3
+        idx = [(k + i) % len(sks) for i in range(n)]
+        k += n
+        msgs = [msg_j(1_000_000 + c * 4 + i, URGENT_SEED) for i in range(n)]
+        sigs = gen_sigs(ctx, [sks[i] for i in idx], msgs)
+        out.append((n, dict(job_first_set=np.array([0, n], np.uint32), sigs=np.frombuffer(sigs, np.uint8),
+                            sig_len=np.full(n, 96, np.uint32), msgs=np.frombuffer(b"".join(msgs), np.uint8),
+                            set_pk_first=np.arange(n + 1, dtype=np.uint32),
+                            pk_index=np.array([work["pk_index"][work["set_pk_first"][i]] for i in idx], np.uint32),
+                            job_flags=np.array([JOB_URGENT], np.uint8), sig_stride=96)))
+    return out
+
+
+def urgent_probe(ctx, ucalls, stop, every_ms, lat):
+    """Submits the urgent calls one after another, every `every_ms`, until `stop` is set; appends (sets, ms, lane)."""
+    i = 0
+    while not stop.is_set():
+        n, kw = ucalls[i % len(ucalls)]
+        t1 = time.perf_counter()
+        res, st = ctx.verify_raw(**kw, seed=URGENT_SEED)
+        lat.append((n, (time.perf_counter() - t1) * 1e3, int(st.urgent_lane)))
+        if res[0] != 1:
+            raise SystemExit(f"urgent call {i} ({n} sets) verified {res[0]}, expected 1")
+        i += 1
+        stop.wait(every_ms / 1e3)
+
+
+def urgent_summary(lat):
+    out = {}
+    for n in (1, 3):
+        x = np.array([ms for k, ms, _ in lat if k == n])
+        if len(x):
+            out[f"{n}_set"] = {"n": int(len(x)), "p50": round(float(np.percentile(x, 50)), 3),
+                               "p99": round(float(np.percentile(x, 99)), 3), "max": round(float(x.max()), 3)}
+    out["on_urgent_lane"] = int(sum(u for _, _, u in lat))
+    return out
 
 
 def parity_leg(ctx, work, pool, calls, expected, table, hc, slots):
@@ -501,6 +550,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--urgent-every-ms", type=float, default=0.0,
+                    help="latency probe: during the timed region one thread submits urgent 1- / 3-set calls "
+                         "(verifyOnMainThread, BLSGPU_JOB_URGENT) this often, and their isolated latency is measured "
+                         "before it (0 = off)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -581,6 +634,23 @@ def main():
     pool = ThreadPoolExecutor(max_workers=max(1, args.inflight, 4 * ctx.get_option("slots") + 4))
     for _ in range(args.warmup):
         list(pool.map(step, range(max(1, args.inflight))))
+    urgent = None
+    if args.urgent_every_ms > 0:
+        import threading
+
+        ucalls = urgent_calls(ctx, work)
+        iso = []
+        for i in range(2 * len(ucalls)):  # isolated: nothing else in flight
+            n, kw = ucalls[i % len(ucalls)]
+            t1 = time.perf_counter()
+            res, st = ctx.verify_raw(**kw, seed=URGENT_SEED)
+            if i >= 4:  # the first calls build the lane's buffers
+                iso.append((n, (time.perf_counter() - t1) * 1e3, int(st.urgent_lane)))
+            assert res[0] == 1
+        urgent = {"isolated_ms": urgent_summary(iso), "every_ms": args.urgent_every_ms,
+                  "urgent_cus": ctx.get_option("urgent_cus"), "urgent_isolate": ctx.get_option("urgent_isolate"),
+                  "urgent_lane_option": ctx.get_option("urgent_lane")}
+        ulat, ustop = [], threading.Event()
     # the untimed isolated calls below use variant 0
 
     def barrier():
@@ -601,7 +671,14 @@ def main():
     sync()
     t0 = time.perf_counter()
     w0 = time.monotonic_ns()  # the timed window on CLOCK_MONOTONIC, the clock of rocprofv3's kernel timestamps
+    if urgent is not None:
+        uthread = threading.Thread(target=urgent_probe, args=(ctx, ucalls, ustop, args.urgent_every_ms, ulat))
+        uthread.start()
     results = list(pool.map(step, range(args.steps)))
+    if urgent is not None:
+        ustop.set()
+        uthread.join()
+        urgent["under_load_ms"] = urgent_summary(ulat)
     sync()
     barrier()
     dt = time.perf_counter() - t0
@@ -649,6 +726,8 @@ def main():
         "call_latency_under_load_ms": {"p50": round(float(np.percentile(call_lat, 50)), 2),
                                        "p99": round(float(np.percentile(call_lat, 99)), 2)},
     }
+    if urgent is not None:
+        out["urgent"] = urgent
     if not args.no_profile:
         runs = [(list(st.stage_ms[:8]), st.run_sets, st.groups, st.unique_messages // n_dev, miller_k_of(st))
                 for st in runs_timed if n_dev == 1]

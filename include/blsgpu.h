@@ -39,7 +39,17 @@
 extern "C" {
 #endif
 
-#define BLSGPU_ABI_VERSION 6
+#define BLSGPU_ABI_VERSION 7
+
+/* blsgpu_batch.job_flags bits (reference VerifySignatureOpts, chain/bls/interface.ts:3-18) */
+#define BLSGPU_JOB_BATCHABLE 1u /* opts.batchable: the job may share a random-linear-combination group */
+#define BLSGPU_JOB_URGENT 2u    /* opts.verifyOnMainThread ("no-delay"): the reference verifies such a job at once on
+                                   the main thread, bypassing the pool queue (multithread/index.ts:138-151; used for the
+                                   gossip block proposer signature, chain/validation/block.ts:146).  A call with an
+                                   urgent job runs on the device's urgent lane: its own dispatcher, slot and streams
+                                   (on a reserved CU partition when option "urgent_cus" > 0), never queued behind or
+                                   merged with throughput calls (option "urgent_lane"; calls above "urgent_max_sets"
+                                   sets go to the head of the device queue instead). */
 
 enum blsgpu_code {
   BLSGPU_OK = 0,
@@ -70,7 +80,7 @@ typedef struct blsgpu_batch {
   uint32_t n_sets;
   uint32_t n_jobs;
   const uint32_t* job_first_set; /* [n_jobs + 1], non-decreasing, job_first_set[n_jobs] == n_sets */
-  const uint8_t* job_flags;      /* [n_jobs] bit0 = batchable (VerifySignatureOpts.batchable); NULL = none */
+  const uint8_t* job_flags;      /* [n_jobs] BLSGPU_JOB_BATCHABLE | BLSGPU_JOB_URGENT; NULL = none */
   /* Public keys, one of three modes (set_pk_first is [n_sets + 1], non-decreasing, starting at 0):
    *  bytes mode (pk_bytes, set_pk_first == NULL): pk_bytes[96 * i] = set i's pubkey, uncompressed affine
    *    (ZCash) -- what the pool sends today, getAggregatedPubkey(set).toBytes() (multithread/index.ts:160);
@@ -116,6 +126,7 @@ typedef struct blsgpu_stats {
   uint32_t fallback_jobs;   /* clean jobs of failed groups re-checked on their own (the run's, like run_sets) */
   uint32_t fallback_miller; /* Miller loops the fallback recomputed: 0 when it reused the batch pass's per-set values
                                (per-set pairings, no same-message units) */
+  uint32_t urgent_lane;     /* 1 = the call ran on a device's urgent lane (BLSGPU_JOB_URGENT) */
 } blsgpu_stats;
 
 /* Create a context on the given HIP devices (NULL / n <= 0: every visible device).  Each device runs
@@ -183,6 +194,13 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * "tail_on_msg" / "copy_stream" (run-formation experiments, 0/1, default 0: a run leaves the pipeline count when its
  * message branch is done / the group stage on the pair's high-priority message stream / the input copy on the table
  * stream),
+ * "urgent_lane" (calls with a BLSGPU_JOB_URGENT job run on the device's urgent lane, 0/1, default 1), "urgent_max_sets"
+ * (larger urgent calls are queued at the head of the device queue instead, default 512), "urgent_excl" (urgent runs
+ * may use the exclusive-CU padding of the cooperative kernels, 0/1, default 0), "urgent_cus" (CUs per device reserved
+ * for the urgent lane's streams, a multiple of 8 up to 128, 0 = no partition: the lane's streams take the highest
+ * priority; CU mask bits [0, urgent_cus), which the driver deals round-robin over the XCDs) and "urgent_isolate" (with a
+ * partition, the pipeline streams are masked off it, 0/1, default 1) -- these two only before the first call (the
+ * streams are created with it; BLSGPU_ERR_ARGS afterwards),
  * "lane_tail_min" / "lane_tail_parts" (runs of >= lane_tail_min sets take lane forms of the Horner passes (bit 0)
  * and of MillerLoop(-g1, S) (bit 1) instead of the cooperative workgroups; default 0 = never, parts 3), "serial"
  * (diagnostics: every branch of a run on one stream, so each kernel runs alone on the chip; 0/1, default 0), "profile" (per-stage kernel times in

@@ -130,6 +130,7 @@ struct Slot {
   bool retire = false;     // set under the device queue lock: the dispatcher exits instead of taking work
   bool in_flight = false;  // the slot's run counts in Device::runs_inflight
   bool alone = false;      // no other run was in flight when the slot took its run
+  bool urgent = false;     // the device's urgent-lane slot (BLSGPU_JOB_URGENT calls): its own streams (Device::ust)
 
   // the stream buffer growth is ordered on (hipFreeAsync / hipMallocAsync); the slot's previous work is complete
   // whenever it grows a buffer (its dispatcher waits for each run), so only this ordering matters
@@ -189,6 +190,17 @@ struct Device {
   int runs_inflight = 0;  // under q_mu: runs taken by a slot whose batch pass has not completed
   std::atomic<uint32_t> run_seq{0};  // run counter: the stream pair of a run (BLSGPU_STREAM_PAIRS)
   std::atomic<int64_t> load{0};  // cost (sets + pubkeys / 256, x256) of the shards queued or running here (routing)
+  // Urgent lane (BLSGPU_JOB_URGENT, the reference's verifyOnMainThread): one slot with its own dispatcher and two stream
+  // pairs, taking urgent calls from uqueue (under q_mu) one at a time.  It never counts in runs_inflight and never takes
+  // enq_mu, so an urgent call waits for no throughput run on the host; on the device its streams either run on a
+  // reserved CU partition that the pipeline streams are masked off ("urgent_cus" > 0) or at the highest priority.
+  hipStream_t ust[4] = {};
+  std::deque<Task> uqueue;
+  Slot* uslot = nullptr;
+  std::thread uworker;
+  std::atomic<int> upending{0};  // urgent calls queued or running here (routing of urgent calls)
+  int urgent_cus = 0;            // CUs of the partition the streams were created with (0 = none)
+  std::vector<uint32_t> main_mask;  // CU mask of the pipeline and fallback streams (empty = all CUs, priorities)
 };
 
 // Device-failure injection (blsgpu_debug_inject, tests only): the next `count` pipeline runs after `skip` more fail as
@@ -235,6 +247,9 @@ struct Options {  // snapshot taken at the start of each call
   int64_t fb_check6 = 2;          // those runs' lane checks: 0 one lane per check; 1 MillerLoop(-g1, S) one lane and the
                                   // final exponentiation six lanes per check (gt6.hpp); 2 both on six lanes
   int64_t fb_force_busy = 0;      // tests: every run's fallback takes the under-load forms
+  int64_t urgent_lane = 1;        // calls with a BLSGPU_JOB_URGENT job run on the device's urgent lane
+  int64_t urgent_max_sets = 512;  // larger urgent calls go to the head of the device queue instead
+  int64_t urgent_excl = 0;        // urgent runs may use the exclusive-CU padding of the cooperative kernels
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
            group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&
@@ -370,6 +385,10 @@ struct blsgpu_ctx {
   std::mutex slots_mu;  // slot creation / resizing
   bool slots_started = false;
   std::atomic<uint32_t> route_seq{0};  // rotating tie-break of route_rule
+  // urgent lane partition (set before the first call: the streams are created with it): CUs per device reserved for
+  // the urgent streams, a multiple of 8; with urgent_isolate the pipeline streams are masked off them
+  int64_t urgent_cus = 0;
+  int64_t urgent_isolate = 1;
 };
 
 namespace {
@@ -631,7 +650,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   const uint32_t n_items = merged ? n_units : n;
   const bool coop = n_items <= (uint32_t)opt.coop_max && opt.miller_k <= 1;
   const bool coop_g2 = n <= (uint32_t)opt.coop_g2_max;
-  const bool excl = BLSGPU_EXCLUSIVE_SMALL && n_items <= (uint32_t)opt.coop_excl_max;
+  // (an urgent run takes the padding only with urgent_excl: on a small CU partition, or beside throughput runs, a
+  // workgroup that needs a whole CU waits for one)
+  const bool excl = BLSGPU_EXCLUSIVE_SMALL && n_items <= (uint32_t)opt.coop_excl_max && (!sl.urgent || opt.urgent_excl);
   const uint32_t mk = coop ? 1u : opt.miller_k > 0 ? (uint32_t)opt.miller_k : miller_k_auto(n_items);
   std::vector<uint32_t> chunk_first{0}, chunk_items, g_chunks(2 * (size_t)ng0);
   chunk_items.reserve(n);
@@ -746,9 +767,12 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   else
     in_bytes = o_pk + (size_t)n * 96;
   const size_t o_pk2 = al256(o_pk + (size_t)(n + 1) * 4);
-  const int par = BLSGPU_STREAM_PAIRS ? (int)(d.run_seq.fetch_add(1) % (uint32_t)d.npairs) : 0;
-  const int other = (par + 1) % d.npairs;
-  hipStream_t s = BLSGPU_STREAM_PAIRS ? d.st[2 * par] : d.st[kSig];
+  // the urgent slot runs on its own two stream pairs (Device::ust), every run on pair 0 with pair 1 idle beside it
+  hipStream_t* const dst = sl.urgent ? d.ust : d.st;
+  const int npairs = sl.urgent ? 2 : d.npairs;
+  const int par = sl.urgent ? 0 : BLSGPU_STREAM_PAIRS ? (int)(d.run_seq.fetch_add(1) % (uint32_t)npairs) : 0;
+  const int other = (par + 1) % npairs;
+  hipStream_t s = BLSGPU_STREAM_PAIRS ? dst[2 * par] : dst[kSig];
   sl.set_stream(s);  // buffer growth of the batch pass, ordered before the input copy on the same stream
   sl.h_in.ensure(in_bytes);
   sl.d_in.ensure(in_bytes);
@@ -896,9 +920,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // A small run that found the device idle puts its pubkey branch on the other pair's (idle) signature stream, beside
   // its own signature decode and subgroup checks instead of in front of them: the signature branch was a small
   // call's critical path (C1 serial trace: 7.25 ms vs the message branch's 6.15).
-  hipStream_t sm = BLSGPU_STREAM_PAIRS ? d.st[2 * par + 1] : d.st[kMsg],
-              sp = BLSGPU_STREAM_PAIRS ? (small && sl.alone ? d.st[2 * other] : s) : d.st[kPk],
-              stl = BLSGPU_STREAM_PAIRS ? s : d.st[kTail];
+  hipStream_t sm = BLSGPU_STREAM_PAIRS ? dst[2 * par + 1] : dst[kMsg],
+              sp = BLSGPU_STREAM_PAIRS ? (small && sl.alone ? dst[2 * other] : s) : dst[kPk],
+              stl = BLSGPU_STREAM_PAIRS ? s : dst[kTail];
   if (opt.serial) sm = sp = stl = s;
   auto beg = [&](int k, hipStream_t st) {
     if (prof) HIPCHK(hipEventRecord(sl.ev[2 * k], st));
@@ -907,7 +931,8 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     if (prof) HIPCHK(hipEventRecord(sl.ev[2 * k + 1], st));
   };
   {
-    std::lock_guard<std::mutex> enq(d.enq_mu);
+    std::unique_lock<std::mutex> enq(d.enq_mu, std::defer_lock);
+    if (!sl.urgent) enq.lock();  // the urgent lane's streams are its own: nothing to keep in order with
     if (host_trace())
       fprintf(stderr,
               "[blsgpu host] run %u sets: merge %.2f ms, prep %.2f ms (dedupe %.2f, structure %.2f), pick-to-copy %.2f "
@@ -916,7 +941,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     // The input copy goes on the run's signature stream, or (copy_stream, when none of the run's buffers was
     // reallocated in that stream's order) on the device's table stream: a previous run's tail still queued on the
     // signature stream of this pair then delays only this run's signature branch, not its message branch
-    const bool own_copy = opt.copy_stream && !opt.serial && tl_async_grow == grow0;
+    const bool own_copy = opt.copy_stream && !opt.serial && !sl.urgent && tl_async_grow == grow0;
     hipStream_t sc = own_copy ? d.table_stream : s;
     HIPCHK(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, sc));
     HIPCHK(hipEventRecord(sl.join_in, sc));
@@ -955,7 +980,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     // enters, and a dropped valid signature is in G2, so its term e(-g1, r sig) != 1) and its jobs are re-checked one
     // by one with exact masks (the fallback), while a clean group's S is exact.  Saves the MSM's ~1.5 ms on the
     // signature branch of a 128-set call.
-    hipStream_t smsm = spec ? d.st[2 * other + 1] : s;
+    hipStream_t smsm = spec ? dst[2 * other + 1] : s;
     PipelineBuffers pbm = pb;
     if (spec) pbm.include = db + ob_spec;
     beg(0, s);
@@ -1338,6 +1363,7 @@ void finish_call(Call* c) {
     local.miller_chunks += c->sst[k].miller_chunks;
     local.fallback_jobs += c->sst[k].fallback_jobs;
     local.fallback_miller += c->sst[k].fallback_miller;
+    local.urgent_lane |= c->sst[k].urgent_lane;
     if (c->rc[k] != BLSGPU_OK && c->rc[k] != BLSGPU_DEVICE_ERROR) status = c->rc[k];
   }
   local.run_sets = c->sst.empty() ? 0 : c->sst[0].run_sets;
@@ -1677,6 +1703,7 @@ void run_task(Device& d, Slot& sl, const Task& t) {
         rc = run_call_shard(d, sl, c->b, sh, c->job_result, c->seed, c->opt, c->max_index, c->sst[t.shard],
                             scal.data());
         c->sst[t.shard].run_calls = 1;
+        c->sst[t.shard].urgent_lane = sl.urgent ? 1 : 0;
       }
     } catch (...) {
       rc = BLSGPU_DEVICE_ERROR;
@@ -1795,6 +1822,31 @@ void worker_loop(Device* d, Slot* sl) {
   }
 }
 
+// The urgent lane's dispatcher: takes urgent calls one at a time, oldest first, and runs each on the lane's own stream
+// pairs (run_shard: Slot::urgent) -- the reference's verifyOnMainThread verifies at once, outside the pool queue
+// (multithread/index.ts:138-151).  `alone` holds for its streams, so a run takes the latency forms of an idle device:
+// the speculative MSM and the pubkey branch on the idle pair, r_i sig_i beside the batch pass, cooperative fallback
+// checks.  Exits when the device stops and its urgent queue is drained.
+void urgent_loop(Device* d, Slot* sl) {
+  tl_dispatcher = true;
+  (void)hipSetDevice(d->id);
+  for (;;) {
+    Task t;
+    {
+      std::unique_lock<std::mutex> lk(d->q_mu);
+      d->q_cv.wait(lk, [&] { return d->stop || !d->uqueue.empty(); });
+      if (d->uqueue.empty()) return;  // stop requested and nothing left
+      t = d->uqueue.front();
+      d->uqueue.pop_front();
+    }
+    sl->alone = true;
+    tl_run_t0 = std::chrono::steady_clock::now();
+    tl_merge_ms = 0;
+    run_task(*d, *sl, t);  // completes the call (it has one shard)
+    d->upending.fetch_sub(1, std::memory_order_relaxed);
+  }
+}
+
 // Frees a slot whose dispatcher has exited (or never started): its buffers (stream-ordered frees on the stream the
 // slot last grew them on, then that stream is drained) and events.
 void free_slot(Device* d, Slot* s) {
@@ -1811,6 +1863,57 @@ void free_slot(Device* d, Slot* s) {
   delete s;
 }
 
+// A stream on the CUs of `mask` (hipExtStreamCreateWithCUMask: its own hardware queue, normal priority), or, with no
+// mask, a non-blocking stream of priority `prio`.
+hipStream_t make_stream(const std::vector<uint32_t>& mask, int prio) {
+  hipStream_t st = nullptr;
+  if (!mask.empty())
+    HIPCHK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  else
+    HIPCHK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
+  return st;
+}
+
+// The device's pipeline streams and its urgent lane's (created with the first call, so "urgent_cus" set after init
+// applies).  The urgent partition is CU mask bits [0, urgent_cus): the driver deals mask bits round-robin over the
+// XCDs (bit i -> XCD i % 8 in SPX mode; measured, profiles/r06_cu_probe.json), so a multiple of 8 bits gives every XCD
+// the same number of partition CUs -- a workgroup is dealt to any XCD, and an XCD without a CU of the stream's mask
+// would never run it.  With isolation the pipeline streams (and the slots' fallback streams) are masked to the
+// complement: the partition then always has free SIMDs for an urgent run, at the cost of those CUs' throughput and of
+// the pipeline streams' priorities (a CU-masked stream has normal priority).  Without a partition the urgent streams
+// take the device's highest priority.
+void create_streams(blsgpu_ctx* ctx, Device* d) {
+  HIPCHK(hipSetDevice(d->id));
+  int prio_lo = 0, prio_hi = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  int n_cu = 0;
+  HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, d->id));
+  const int part = (int)std::min<int64_t>(ctx->urgent_cus, n_cu / 2) & ~7;
+  d->urgent_cus = part;
+  std::vector<uint32_t> pmask;
+  d->main_mask.clear();
+  if (part > 0) {
+    pmask.assign((size_t)(n_cu + 31) / 32, 0);
+    d->main_mask.assign((size_t)(n_cu + 31) / 32, 0);
+    for (int i = 0; i < n_cu; i++) (i < part ? pmask : d->main_mask)[i / 32] |= 1u << (i % 32);
+    if (!ctx->urgent_isolate) d->main_mask.clear();
+  }
+  // The message branch (hash_to_G2 -> Miller lines -> Miller accumulation -> F reduction) is the serial chain that
+  // bounds a device's throughput (~70% of the work, one in-order stream shared by the runs in flight): its stream
+  // gets the device's highest priority, so its kernels take free SIMDs first and the signature / pubkey branches
+  // fill the gaps its tails leave, instead of stretching the chain; so does the short tail (final
+  // exponentiations -> results), which returns finished calls sooner.  (C2, interleaved A/B: 2.90M sets/s with no
+  // priorities, 2.94M message stream, 2.945M message + tail; profiles/r03_ab6_stream_priority.txt.)
+  // A third stream pair when the process has the hardware queues for it (GPU_MAX_HW_QUEUES >= 6): each of the
+  // default three slots' runs then has its own pair, and a run never queues behind another run's tail.
+  d->npairs = ctx->hw_queues >= 6 ? kMaxPairs : 2;
+  for (int k = 0; k < 2 * d->npairs; k++) {
+    const bool high = (BLSGPU_STREAM_PRIO & (1 << (k & 3))) != 0 || (k >= kStreams && (k & 1));
+    d->st[k] = make_stream(d->main_mask, high ? prio_hi : prio_lo);
+  }
+  for (int k = 0; k < 4; k++) d->ust[k] = make_stream(pmask, prio_hi);
+}
+
 void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet shared)
   Slot* s = new Slot();
   HIPCHK(hipSetDevice(d->id));
@@ -1822,7 +1925,7 @@ void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet sh
     for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
     int prio_lo = 0, prio_hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    HIPCHK(hipStreamCreateWithPriority(&s->fb, hipStreamNonBlocking, prio_lo));
+    s->fb = make_stream(d->main_mask, prio_lo);
   } catch (HipError&) {
     free_slot(d, s);
     throw;
@@ -1868,9 +1971,13 @@ void destroy_device(Device* d) {
   }
   d->q_cv.notify_all();
   for (auto& t : d->workers) t.join();
+  if (d->uworker.joinable()) d->uworker.join();
   for (Slot* s : d->slots) free_slot(d, s);
+  if (d->uslot) free_slot(d, d->uslot);
   (void)hipSetDevice(d->id);
   for (hipStream_t st : d->st)
+    if (st) (void)hipStreamSynchronize(st), (void)hipStreamDestroy(st);
+  for (hipStream_t st : d->ust)
     if (st) (void)hipStreamSynchronize(st), (void)hipStreamDestroy(st);
   d->helper.release_all();
   d->table.release();
@@ -1896,7 +2003,32 @@ int ensure_slots(blsgpu_ctx* ctx) {
   std::lock_guard<std::mutex> lk(ctx->slots_mu);
   if (ctx->slots_started) return BLSGPU_OK;
   try {
-    for (Device* d : ctx->devs) resize_slots(d, ctx->slots_per_device);
+    for (Device* d : ctx->devs) {
+      if (!d->st[0]) create_streams(ctx, d);
+      resize_slots(d, ctx->slots_per_device);
+      if (!d->uslot) {  // the urgent lane: one slot, its own dispatcher
+        Slot* u = new Slot();
+        u->urgent = true;
+        try {
+          u->set_stream(d->ust[0]);
+          for (hipEvent_t* e : {&u->join_in, &u->join_msg, &u->join_pk, &u->join_mask, &u->join_gsm, &u->join_dec,
+                                &u->join_msm, &u->join_rsig, &u->done})
+            HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+          for (auto& e : u->ev) HIPCHK(hipEventCreate(&e));
+        } catch (HipError&) {
+          free_slot(d, u);
+          throw;
+        }
+        d->uslot = u;  // fallback on its own signature stream (Slot::fb null)
+        try {
+          d->uworker = std::thread(urgent_loop, d, u);
+        } catch (std::system_error&) {
+          d->uslot = nullptr;
+          free_slot(d, u);
+          return BLSGPU_DEVICE_ERROR;
+        }
+      }
+    }
   } catch (HipError&) {
     return BLSGPU_DEVICE_ERROR;
   }
@@ -1911,8 +2043,45 @@ int64_t shard_cost(const blsgpu_batch& b, const Shard& sh) {
   return c;
 }
 
+// An urgent call (a BLSGPU_JOB_URGENT job) of <= urgent_max_sets sets goes whole to the urgent lane of the device with
+// the fewest urgent calls pending (ties rotate); a larger one is routed as any call but queued at the head of each
+// device's queue.  Returns true when the call was queued on an urgent lane.
+bool launch_urgent(blsgpu_ctx* ctx, Call* c) {
+  const blsgpu_batch& b = c->b;
+  const uint32_t nd = (uint32_t)std::min<int64_t>((int64_t)ctx->devs.size(), c->opt.max_devices);
+  if (!c->opt.urgent_lane || (int64_t)b.n_sets > c->opt.urgent_max_sets || nd == 0) return false;
+  const uint32_t start = ctx->route_seq.fetch_add(1, std::memory_order_relaxed) % nd;
+  uint32_t best = start;
+  for (uint32_t k = 1; k < nd; k++) {
+    const uint32_t x = (start + k) % nd;
+    if (ctx->devs[x]->upending.load(std::memory_order_relaxed) < ctx->devs[best]->upending.load(std::memory_order_relaxed))
+      best = x;
+  }
+  Device* d = ctx->devs[best];
+  if (!d->uslot) return false;
+  Shard sh{0, b.n_jobs, 0, b.n_sets};
+  sh.dev = best;
+  sh.cost = 0;
+  c->shards.push_back(sh);
+  c->sst.assign(1, blsgpu_stats{});
+  c->rc.assign(1, BLSGPU_OK);
+  c->remaining = 1;
+  c->t0 = std::chrono::steady_clock::now();
+  d->upending.fetch_add(1, std::memory_order_relaxed);
+  {
+    std::lock_guard<std::mutex> lk(d->q_mu);
+    d->uqueue.push_back({c, 0});
+  }
+  d->q_cv.notify_all();
+  return true;
+}
+
 void launch_call(blsgpu_ctx* ctx, Call* c) {
   const blsgpu_batch& b = c->b;
+  bool urgent = false;
+  if (b.job_flags)
+    for (uint32_t j = 0; j < b.n_jobs && !urgent; j++) urgent = (b.job_flags[j] & BLSGPU_JOB_URGENT) != 0;
+  if (urgent && launch_urgent(ctx, c)) return;
   const uint32_t nd_all = (uint32_t)std::min<int64_t>((int64_t)ctx->devs.size(), c->opt.max_devices);
   std::vector<int64_t> load(nd_all);
   for (uint32_t d = 0; d < nd_all; d++) load[d] = ctx->devs[d]->load.load(std::memory_order_relaxed);
@@ -1937,7 +2106,10 @@ void launch_call(blsgpu_ctx* ctx, Call* c) {
     d->load.fetch_add(c->shards[k].cost, std::memory_order_relaxed);
     {
       std::lock_guard<std::mutex> lk(d->q_mu);
-      d->queue.push_back({c, k});
+      if (urgent)  // too large for the urgent lane: ahead of every queued call
+        d->queue.push_front({c, k});
+      else
+        d->queue.push_back({c, k});
     }
     d->q_cv.notify_all();  // a lingering slot (merge_wait_us) must see it, not only an idle one
   }
@@ -1994,21 +2166,7 @@ int blsgpu_init(const int* devices, int n_devices, blsgpu_ctx** out) {
       ctx->devs.push_back(d);
       HIPCHK(hipSetDevice(id));
       HIPCHK(hipStreamCreateWithFlags(&d->table_stream, hipStreamNonBlocking));
-      // The message branch (hash_to_G2 -> Miller lines -> Miller accumulation -> F reduction) is the serial chain that
-      // bounds a device's throughput (~70% of the work, one in-order stream shared by the runs in flight): its stream
-      // gets the device's highest priority, so its kernels take free SIMDs first and the signature / pubkey branches
-      // fill the gaps its tails leave, instead of stretching the chain; so does the short tail (final
-      // exponentiations -> results), which returns finished calls sooner.  (C2, interleaved A/B: 2.90M sets/s with no
-      // priorities, 2.94M message stream, 2.945M message + tail; profiles/r03_ab6_stream_priority.txt.)
-      int prio_lo = 0, prio_hi = 0;
-      HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-      // a third stream pair when the process has the hardware queues for it (GPU_MAX_HW_QUEUES >= 6): each of the
-      // default three slots' runs then has its own pair, and a run never queues behind another run's tail
-      d->npairs = ctx->hw_queues >= 6 ? kMaxPairs : 2;
-      for (int k = 0; k < 2 * d->npairs; k++) {
-        const bool high = (BLSGPU_STREAM_PRIO & (1 << (k & 3))) != 0 || (k >= kStreams && (k & 1));
-        HIPCHK(hipStreamCreateWithPriority(&d->st[k], hipStreamNonBlocking, high ? prio_hi : prio_lo));
-      }
+      // (the pipeline and urgent streams are created with the first call: create_streams)
     }
   } catch (HipError&) {
     blsgpu_destroy(ctx);
@@ -2079,12 +2237,14 @@ int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* 
           DevBuf<uint32_t> nt;
           nt.ensure((size_t)std::max<uint32_t>(need, d->table_n + d->table_n / 2) * W_PKTAB);
           if (d->table_n)
-            HIPCHK(hipMemcpy(nt.p, d->table.p, (size_t)d->table_n * W_PKTAB * 4, hipMemcpyDeviceToDevice));
+            HIPCHK(hipMemcpyAsync(nt.p, d->table.p, (size_t)d->table_n * W_PKTAB * 4, hipMemcpyDeviceToDevice, ts));
           d->table.release();
           d->table = nt;
         }
-        HIPCHK(hipMemcpy(d->table.p + (size_t)first_index * W_PKTAB, tmp, (size_t)n * W_PKTAB * 4,
-                         hipMemcpyDeviceToDevice));
+        // (on the table stream: a null-stream copy would also wait for the CU-masked streams, which are blocking)
+        HIPCHK(hipMemcpyAsync(d->table.p + (size_t)first_index * W_PKTAB, tmp, (size_t)n * W_PKTAB * 4,
+                              hipMemcpyDeviceToDevice, ts));
+        HIPCHK(hipStreamSynchronize(ts));
         d->table_n = std::max(d->table_n, need);
       }
       (void)hipFree(dpk);
@@ -2116,6 +2276,17 @@ int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* 
 int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return BLSGPU_ERR_ARGS;
   std::string k(key);
+  if (k == "urgent_cus" || k == "urgent_isolate") {  // stream creation: before the first call only
+    std::lock_guard<std::mutex> sk(ctx->slots_mu);
+    if (ctx->slots_started) return BLSGPU_ERR_ARGS;
+    if (k == "urgent_cus") {
+      if (value < 0 || value > 128 || (value & 7)) return BLSGPU_ERR_ARGS;
+      ctx->urgent_cus = value;
+    } else {
+      ctx->urgent_isolate = value != 0;
+    }
+    return BLSGPU_OK;
+  }
   if (k == "slots") {
     // not from a dispatcher thread (a done callback): retiring its own slot would join itself
     if (value < 1 || value > 64 || tl_dispatcher) return BLSGPU_ERR_ARGS;
@@ -2198,6 +2369,13 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
     ctx->opt.fb_lane_min = value;
   } else if (k == "fb_force_busy") {
     ctx->opt.fb_force_busy = value != 0;
+  } else if (k == "urgent_lane") {
+    ctx->opt.urgent_lane = value != 0;
+  } else if (k == "urgent_max_sets") {
+    if (value < 0) return BLSGPU_ERR_ARGS;
+    ctx->opt.urgent_max_sets = value;
+  } else if (k == "urgent_excl") {
+    ctx->opt.urgent_excl = value != 0;
   } else if (k == "fb_check6") {
     if (value < 0 || value > 2) return BLSGPU_ERR_ARGS;
     ctx->opt.fb_check6 = value;
@@ -2249,6 +2427,15 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
     *value = ctx->hw_queues;
     return BLSGPU_OK;
   }
+  if (k == "urgent_cus" || k == "urgent_isolate") {
+    std::lock_guard<std::mutex> sk(ctx->slots_mu);
+    // once the streams exist: the partition device 0 was created with (0 when the device is too small for it)
+    if (k == "urgent_cus")
+      *value = ctx->slots_started && !ctx->devs.empty() ? ctx->devs[0]->urgent_cus : ctx->urgent_cus;
+    else
+      *value = ctx->urgent_isolate;
+    return BLSGPU_OK;
+  }
   if (k == "abi_version") {
     *value = BLSGPU_ABI_VERSION;
     return BLSGPU_OK;
@@ -2290,6 +2477,9 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "fb_direct_min") *value = o.fb_direct_min;
   else if (k == "fb_check6") *value = o.fb_check6;
   else if (k == "fb_force_busy") *value = o.fb_force_busy;
+  else if (k == "urgent_lane") *value = o.urgent_lane;
+  else if (k == "urgent_max_sets") *value = o.urgent_max_sets;
+  else if (k == "urgent_excl") *value = o.urgent_excl;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }

@@ -22,6 +22,9 @@ ERR_ARGS = 100
 ERR_NO_DEVICE = 101
 ERR_CLOSED = 102
 ERR_ENTROPY = 103
+# blsgpu_batch.job_flags bits
+JOB_BATCHABLE = 1
+JOB_URGENT = 2  # VerifySignatureOpts.verifyOnMainThread: the device's urgent lane
 # blsgpu_debug_inject targets
 INJECT_ENTROPY = 1
 INJECT_DEVICE = 2
@@ -83,6 +86,7 @@ class Stats(ctypes.Structure):
         ("run_calls", ctypes.c_uint32),
         ("fallback_jobs", ctypes.c_uint32),
         ("fallback_miller", ctypes.c_uint32),
+        ("urgent_lane", ctypes.c_uint32),
     ]
 
 

@@ -52,6 +52,10 @@ const MAX_BUFFER_WAIT_MS = 100; // multithread/index.ts:57
 const QUEUE_ABORTED = "QUEUE_ERROR_QUEUE_ABORTED"; // util/queue/errors.ts QueueErrorCode.QUEUE_ABORTED
 const SIG_STRIDE = 192;
 
+// job flags (include/blsgpu.h BLSGPU_JOB_*)
+const JOB_BATCHABLE = 1;
+const JOB_URGENT = 2;
+
 // job codes (include/blsgpu.h enum blsgpu_code)
 const CODE_EMPTY_AGGREGATE = 9;
 const CODE_EMPTY_SET = 10;
@@ -145,7 +149,8 @@ class BlsGpuVerifier {
           this.flushBuffered();
         }
       } else if (opts.verifyOnMainThread) {
-        // latency-critical (block proposal, interface.ts:8-17): no buffering at all
+        // latency-critical (block proposal, interface.ts:8-17): no buffering at all, and on the device the urgent
+        // lane (BLSGPU_JOB_URGENT)
         job.mainThread = true;
         this.dispatch([job]);
       } else {
@@ -254,7 +259,9 @@ class BlsGpuVerifier {
     const m = this.metrics && this.metrics.blsThreadPool;
     jobs.forEach((j, ji) => {
       jobFirstSet[ji] = i;
-      jobFlags[ji] = j.batchable ? 1 : 0;
+      // BLSGPU_JOB_BATCHABLE, and BLSGPU_JOB_URGENT for verifyOnMainThread jobs: the runtime runs those on the
+      // device's urgent lane, never queued behind or merged with the gossip flood (multithread/index.ts:138-151)
+      jobFlags[ji] = (j.batchable ? JOB_BATCHABLE : 0) | (j.mainThread ? JOB_URGENT : 0);
       if (m && m.jobWaitTime && j.addedTimeMs) m.jobWaitTime.observe((now - j.addedTimeMs) / 1000);
       for (const s of j.sets) {
         msgs.set(s.msg.subarray(0, 32), 32 * i);
@@ -290,6 +297,7 @@ class BlsGpuVerifier {
         st.batchRetries += out.batchRetries;
         st.batchSigsSuccess += out.batchSigsSuccess;
         st.uniqueMessages += out.uniqueMessages;
+        if (out.urgentLane) st.urgentCalls = (st.urgentCalls || 0) + 1;
         let okSets = 0;
         let errSets = 0;
         jobs.forEach((j, ji) => (out.results[ji] < 0 ? (errSets += j.sets.length) : (okSets += j.sets.length)));
@@ -395,5 +403,7 @@ module.exports = {
   SignatureSetType,
   MAX_BUFFERED_SIGS,
   MAX_BUFFER_WAIT_MS,
+  JOB_BATCHABLE,
+  JOB_URGENT,
   addon,
 };

@@ -14,13 +14,16 @@
  *   pubkeysCount(ctx) -> number                                   blsgpu_pubkeys_count
  *   setOption(ctx, key, value)                                    blsgpu_set_option
  *   codeName(code) -> string                                      blsgpu_code_name
- *   submit(ctx, req) -> Promise<{results: Int8Array, groups, batchRetries, batchSigsSuccess, deviceMs}>
- *     req = {jobFirstSet: Uint32Array, jobFlags?: Uint8Array, pkBytes?: Uint8Array,
+ *   submit(ctx, req) -> Promise<{results: Int8Array, groups, batchRetries, batchSigsSuccess, deviceMs, ...,
+ *                                 urgentLane}>
+ *     req = {jobFirstSet: Uint32Array, jobFlags?: Uint8Array (BLSGPU_JOB_BATCHABLE 1 | BLSGPU_JOB_URGENT 2),
+ *            pkBytes?: Uint8Array,
  *            setPkFirst?: Uint32Array, pkIndex?: Uint32Array, msgs: Uint8Array, sigs: Uint8Array,
  *            sigLen: Uint32Array, sigStride: number, seed?: number}              blsgpu_submit
  *     (pkBytes alone: one 96-B key per set; pkBytes + setPkFirst: bytes-aggregate; setPkFirst + pkIndex:
  *      device table)
  *   keyValidate(ctx, Uint8Array, pkLen) -> {pk96, status}        blsgpu_key_validate (synchronous)
+ *   debugInject(what, skip, count)                                blsgpu_debug_inject (only with BLSGPU_FAULT_INJECTION=1)
  */
 #define NAPI_VERSION 6
 #include <node_api.h>
@@ -288,6 +291,7 @@ static void settle_on_main(napi_env env, napi_value js_cb, void* context, void* 
       set_num(env, out, "deviceMs", c->stats.device_ms);
       set_num(env, out, "uniqueMessages", c->stats.unique_messages);
       set_num(env, out, "pairingUnits", c->stats.pairing_units);
+      set_num(env, out, "urgentLane", c->stats.urgent_lane);
       napi_resolve_deferred(env, c->deferred, out);
     }
   }
@@ -445,13 +449,17 @@ static napi_value ModuleInit(napi_env env, napi_value exports) {
       {"codeName", NULL, CodeName, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"submit", NULL, Submit, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
       {"keyValidate", NULL, KeyValidate, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
-      {"debugInject", NULL, DebugInject, NULL, NULL, NULL, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), NULL},
   };
-  /* the fault-injection test hook is exported only to processes started with BLSGPU_FAULT_INJECTION=1 (the library
-   * refuses to arm it otherwise) */
+  napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
+  /* the fault-injection test hook is exported, by its own definition, only to processes started with
+   * BLSGPU_FAULT_INJECTION=1 (the library refuses to arm it otherwise) */
   const char* fi = getenv("BLSGPU_FAULT_INJECTION");
-  const int with_inject = fi && fi[0] == '1' && fi[1] == 0;
-  napi_define_properties(env, exports, sizeof props / sizeof props[0] - (with_inject ? 0 : 1), props);
+  if (fi && fi[0] == '1' && fi[1] == 0) {
+    napi_property_descriptor inject = {"debugInject", NULL, DebugInject, NULL, NULL, NULL,
+                                       (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable),
+                                       NULL};
+    napi_define_properties(env, exports, 1, &inject);
+  }
   napi_value v;
   napi_create_int32(env, BLSGPU_ABI_VERSION, &v);
   napi_set_named_property(env, exports, "abiVersion", v);

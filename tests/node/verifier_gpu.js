@@ -6,7 +6,8 @@
 //     other concurrent calls (multithread.test.ts:89-106);
 //   - more than 32 buffered batchable sets flush without waiting for the 100 ms timer;
 //   - close() rejects buffered jobs with QUEUE_ERROR_QUEUE_ABORTED.
-// Usage: node tests/node/verifier_gpu.js   (exit code 0 = pass; prints one line per check)
+// Usage: BLSGPU_FAULT_INJECTION=1 node tests/node/verifier_gpu.js   (exit code 0 = pass; one line per check; without
+// the variable the addon does not export debugInject and the fault-injection checks are skipped)
 const assert = require("assert");
 const fs = require("fs");
 const path = require("path");
@@ -112,9 +113,16 @@ async function main() {
   assert.ok(res.every((x) => x === true));
   console.log(`ok 40 buffered batchable calls in ${Date.now() - t0} ms, stats ${JSON.stringify(v.stats)}`);
 
-  // verifyOnMainThread path (no buffering)
+  // verifyOnMainThread path (no buffering; BLSGPU_JOB_URGENT: the device's urgent lane, multithread/index.ts:138-151)
+  const urgentBefore = v.stats.urgentCalls || 0;
   assert.strictEqual(await v.verifySignatureSets(valid.slice(0, 3), {verifyOnMainThread: true}), true);
-  console.log("ok verifyOnMainThread");
+  assert.strictEqual(await v.verifySignatureSets(valid.slice(3, 4), {verifyOnMainThread: true}), true);
+  assert.strictEqual(v.stats.urgentCalls - urgentBefore, 2, "verifyOnMainThread calls ran on the urgent lane");
+  // a batchable call is not urgent
+  const urgentMid = v.stats.urgentCalls;
+  assert.strictEqual(await v.verifySignatureSets(valid.slice(0, 1), {batchable: true}), true);
+  assert.strictEqual(v.stats.urgentCalls, urgentMid);
+  console.log("ok verifyOnMainThread (urgent lane)");
 
   // aggregate sets of plain PublicKey objects (no registration): bytes-aggregate mode on the GPU -- the gossip
   // attestation call (attestation.ts:131-138), every golden case
@@ -184,8 +192,10 @@ async function main() {
 
   // a device failure rejects every job of the call with the device status, never `false` (index.ts:368-375), and
   // the verifier keeps serving: the next call verifies (fault injection: blsgpu_debug_inject)
-  {
-    const {addon} = require(path.join(ROOT, "lodestar_amd", "node", "BlsGpuVerifier.cjs"));
+  const {addon} = require(path.join(ROOT, "lodestar_amd", "node", "BlsGpuVerifier.cjs"));
+  if (typeof addon.debugInject !== "function") {
+    console.log("skip fault injection (run with BLSGPU_FAULT_INJECTION=1)");
+  } else {
     addon.debugInject(2, 0, 1);
     const outs = await Promise.all([
       settle(v.verifySignatureSets(valid.slice(0, 3), {verifyOnMainThread: true})),
