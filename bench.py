@@ -394,6 +394,48 @@ def oracle_table(work):
     return cpu.Table(work["_table_pks"]) if "_table_pks" in work else None
 
 
+def concat_calls(calls):
+    """One batch of several calls' jobs (same pubkey mode): the reference pool keeps all its workers busy with the
+    calls in flight, so the all-core baseline verifies enough jobs at once for every thread to hold a request."""
+    out = {"sig_stride": calls[0]["sig_stride"]}
+    jfs, spf, off, koff = [np.zeros(1, np.uint32)], [np.zeros(1, np.uint32)], 0, 0
+    for c in calls:
+        jfs.append(np.asarray(c["job_first_set"][1:], np.uint32) + off)
+        if c.get("set_pk_first") is not None:
+            spf.append(np.asarray(c["set_pk_first"][1:], np.uint32) + koff)
+            koff += int(c["set_pk_first"][-1])
+        off += int(c["job_first_set"][-1])
+    out["job_first_set"] = np.concatenate(jfs)
+    if calls[0].get("set_pk_first") is not None:
+        out["set_pk_first"] = np.concatenate(spf)
+    for k in ("sigs", "sig_len", "msgs", "job_flags", "pk_index", "pk_bytes"):
+        if calls[0].get(k) is not None:
+            out[k] = np.concatenate([np.asarray(c[k]) for c in calls])
+    return out
+
+
+def cpu_baseline_all_cores(calls, expected, table, hc):
+    """The port on every CPU of the affinity mask -- the reference pool's size, os.cpus().length
+    (multithread/poolSize.ts:7) -- over as many in-flight calls as give each thread a >= 128-set worker request."""
+    from oracle import cpu
+
+    threads = hc["affinity_cpus"]
+    n_sets = int(calls[0]["job_first_set"][-1])
+    k = max(1, min(len(calls), -(-threads * 128 // max(n_sets, 1)), 65536 // max(n_sets, 1)))
+    batch = concat_calls(calls[:k])
+    t0 = time.perf_counter()
+    res, st = cpu.verify_jobs(table=table, threads=threads, **batch)
+    dt = time.perf_counter() - t0
+    agree = bool(np.array_equal(res, np.concatenate([expected] * k)))
+    return {"value": round(k * n_sets / dt, 2), "unit": "sets/s", "cores": threads, "kind": "port",
+            "sample": f"{k} in-flight steps ({k * n_sets} sets, {st.work_requests} worker requests) through "
+                      f"oracle/blscpu.c on all {threads} CPUs of the affinity mask "
+                      f"({hc['affinity_physical_cores']} physical cores), {dt:.2f} s, results "
+                      f"{'identical to' if agree else 'DIFFERENT from'} the GPU's",
+            "results_match_gpu": agree,
+            "blst_anchor_sets_per_s": BLST_SETS_PER_CORE * (hc["affinity_physical_cores"] or threads)}
+
+
 def cpu_baseline(call, expected, table, hc):
     """The reference pool restated in C (oracle/blscpu.c: 6 x 64-bit Montgomery, the pool's job split, >= 16-job
     batch chunks and per-job fallback; kind "port") on this host's cores, on the SAME step the GPU times (all of
@@ -550,6 +592,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--devices-same", type=int, default=-1,
+                    help="host-capacity mode: the --gpus N in-process device contexts all on this one device (N "
+                         "dispatcher sets and stream sets on one GPU; throughput is one GPU's, the host cost is N's)")
     ap.add_argument("--urgent-every-ms", type=float, default=0.0,
                     help="latency probe: during the timed region one thread submits urgent 1- / 3-set calls "
                          "(verifyOnMainThread, BLSGPU_JOB_URGENT) this often, and their isolated latency is measured "
@@ -574,6 +619,8 @@ def main():
     # (each call sharded over them by the runtime)
     n_dev = args.gpus if world == 1 else 1
     devices = list(range(n_dev)) if world == 1 else [local_rank]
+    if args.devices_same >= 0 and world == 1:
+        devices = [args.devices_same] * n_dev
     ctx = Context(devices)
     ctx.set_option("group_sets", args.group_sets)
     ctx.set_option("group_policy", args.group_policy)
@@ -670,6 +717,7 @@ def main():
     barrier()
     sync()
     t0 = time.perf_counter()
+    cpu0 = time.process_time()  # host CPU seconds of every thread of the process (dispatchers, packing, callers)
     w0 = time.monotonic_ns()  # the timed window on CLOCK_MONOTONIC, the clock of rocprofv3's kernel timestamps
     if urgent is not None:
         uthread = threading.Thread(target=urgent_probe, args=(ctx, ucalls, ustop, args.urgent_every_ms, ulat))
@@ -682,6 +730,7 @@ def main():
     sync()
     barrier()
     dt = time.perf_counter() - t0
+    cpu_s = time.process_time() - cpu0
     w1 = time.monotonic_ns()
     ctx.set_option("profile", 0)
     stats = [r[0] for r in results]
@@ -723,6 +772,13 @@ def main():
                        pipeline_runs_timed=len(runs_timed),
                        parallelism=f"shard-by-job x{n_gpus} ({'one process per GPU' if world > 1 else 'in-process devices'}), no collective"),
         "p50_batch_latency_ms": round(float(np.median(lat)), 3),
+        # host cost of the timed region: CPU seconds of the whole process per million sets verified, and each run's
+        # host time from its slot taking it to its input copy (blsgpu_stats.host_ms)
+        "host": {"cpu_s_per_million_sets": round(cpu_s / (total_sets / 1e6), 4), "process_cpu_s": round(cpu_s, 3),
+                 "run_host_ms": {"p50": round(float(np.percentile([st.host_ms for st in runs_timed], 50)), 3),
+                                 "p99": round(float(np.percentile([st.host_ms for st in runs_timed], 99)), 3),
+                                 "runs": len(runs_timed)} if runs_timed else None,
+                 "devices": devices},
         "call_latency_under_load_ms": {"p50": round(float(np.percentile(call_lat, 50)), 2),
                                        "p99": round(float(np.percentile(call_lat, 99)), 2)},
     }
@@ -746,6 +802,8 @@ def main():
             out["parity"] = parity_leg(ctx, work, pool, calls, expected, table, hc, ctx.get_option("slots"))
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(call, expected, table, hc)
+            if hc["affinity_cpus"] > hc["threads"]:
+                out["cpu_baseline"]["all_cores"] = cpu_baseline_all_cores(calls, expected, table, hc)
     out["workload_variants"] = {"count": n_var, "gen_s": round(t_gen, 2)}
     out["timed_window_monotonic_ns"] = [w0, w1]  # tools/occupancy.py --window: the timed steps' kernels in a trace
     if rank == 0:

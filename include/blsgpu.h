@@ -127,6 +127,8 @@ typedef struct blsgpu_stats {
   uint32_t fallback_miller; /* Miller loops the fallback recomputed: 0 when it reused the batch pass's per-set values
                                (per-set pairings, no same-message units) */
   uint32_t urgent_lane;     /* 1 = the call ran on a device's urgent lane (BLSGPU_JOB_URGENT) */
+  double host_ms;           /* host time of the run (like run_sets): from the slot taking it (merging, packing, job
+                               structure, dedupe) to its input copy being queued; the largest over the call's shards */
 } blsgpu_stats;
 
 /* Create a context on the given HIP devices (NULL / n <= 0: every visible device).  Each device runs
@@ -199,7 +201,8 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * may use the exclusive-CU padding of the cooperative kernels, 0/1, default 0), "urgent_cus" (CUs per device reserved
  * for the urgent lane's streams, a multiple of 8 up to 128, 0 = no partition: the lane's streams take the highest
  * priority; CU mask bits [0, urgent_cus), which the driver deals round-robin over the XCDs) and "urgent_isolate" (with a
- * partition, the pipeline streams are masked off it, 0/1, default 1) -- these two only before the first call (the
+ * partition, the pipeline streams are masked off it; 2: and the urgent streams are left unmasked at the highest
+ * priority, so an idle chip is theirs too; 3, diagnostics: the pipeline streams masked with every CU; 0..3) -- these two only before the first call (the
  * streams are created with it; BLSGPU_ERR_ARGS afterwards),
  * "lane_tail_min" / "lane_tail_parts" (runs of >= lane_tail_min sets take lane forms of the Horner passes (bit 0)
  * and of MillerLoop(-g1, S) (bit 1) instead of the cooperative workgroups; default 0 = never, parts 3), "serial"

@@ -109,8 +109,10 @@ constexpr size_t kMillerLineWords = (size_t)MILLER_STEPS * W_LINE;
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// One runtime slot: a dispatcher's staging and work buffers and its events.  The HIP streams belong to the device
-// (Device::st) and are shared by its slots, so a device needs kStreams hardware queues whatever its slot count.
+// One runtime slot: a dispatcher's staging and work buffers and its events.  The pipeline streams belong to the device
+// (Device::st) and are shared by its slots; each slot adds its own fallback stream (Slot::fb).  Under HIP's default of
+// 4 hardware queues a process's streams share queues (HIP deals streams over its queues), so a fallback stream may
+// share a queue with a pipeline stream; CU-masked streams (urgent partition, create_streams) get queues of their own.
 struct Slot {
   hipEvent_t join_in = nullptr, join_msg = nullptr, join_pk = nullptr, join_mask = nullptr, join_gsm = nullptr,
              join_dec = nullptr, join_msm = nullptr, join_rsig = nullptr, done = nullptr;  // no timing
@@ -933,6 +935,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   {
     std::unique_lock<std::mutex> enq(d.enq_mu, std::defer_lock);
     if (!sl.urgent) enq.lock();  // the urgent lane's streams are its own: nothing to keep in order with
+    st.host_ms = ms_since(tl_run_t0);  // the slot picked the run -> its input copy is queued
     if (host_trace())
       fprintf(stderr,
               "[blsgpu host] run %u sets: merge %.2f ms, prep %.2f ms (dedupe %.2f, structure %.2f), pick-to-copy %.2f "
@@ -1181,8 +1184,11 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       rf[2 * q] = cr.first;
       rf[2 * q + 1] = cr.second;
     }
-    // per-set scalings instead of per-job MSMs (or the speculative batch-pass scalings, when the run made them)
-    const bool small_jobs = rsig_spec || rset.size() < (size_t)32 * nr;
+    // per-set scalings instead of per-job MSMs while the jobs are small (a 1-3-set job would leave a 128-lane MSM
+    // workgroup idle); the speculative batch-pass scalings (rsig_spec) then save the scaling launch.  Large retried jobs
+    // (e.g. two failing 1k-set block jobs) take the bucket MSM and the wave-per-job reduce even when the run made the
+    // scalings: one lane summing a job's thousands of r_i sig_i and multiplying its Fp12 values in series is slower.
+    const bool small_jobs = rset.size() < (size_t)32 * nr;
     // A small run (cooperative forms: the chip is far from full) checks every retried job directly in ONE launch --
     // up to kFbDirectMax checks run side by side (4 cooperative workgroups per CU) -- instead of sub-groups, a host
     // round trip and then the jobs of the failing sub-groups: one check round instead of two.  (Cooperative checks slow
@@ -1262,7 +1268,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     st.fallback_jobs += nr;
     if (small_jobs) {
       // r_i sig_i for the retried sets (G2 window tables and results in the fallback's own buffers), unless the batch
-      // pass already formed them (rsig_spec)
+      // pass already formed them (rsig_spec: every set of the run, by set index)
       if (!rsig_spec) sl.d_fb.ensure((size_t)stride * 9 * W_G2J);
       pr.rsig = sl.d_fb.p;
       pr.scal_tab = sl.d_fb.p + (size_t)stride * W_G2J;
@@ -1364,6 +1370,7 @@ void finish_call(Call* c) {
     local.fallback_jobs += c->sst[k].fallback_jobs;
     local.fallback_miller += c->sst[k].fallback_miller;
     local.urgent_lane |= c->sst[k].urgent_lane;
+    local.host_ms = std::max(local.host_ms, c->sst[k].host_ms);
     if (c->rc[k] != BLSGPU_OK && c->rc[k] != BLSGPU_DEVICE_ERROR) status = c->rc[k];
   }
   local.run_sets = c->sst.empty() ? 0 : c->sst[0].run_sets;
@@ -1633,16 +1640,26 @@ void run_merged(Device& d, Slot& sl, const std::vector<Task>& parts, std::vector
       }
     };
     {  // parts of >= 4,096 sets on their own threads (a small part packs faster than a thread starts)
-      std::vector<std::thread> th;
-      for (size_t q = 1; q < live.size(); q++) {
-        const Shard& sh = parts[live[q]].call->shards[parts[live[q]].shard];
-        if (sh.set_end - sh.set_begin >= 4096) th.emplace_back(pack, q);
-      }
+      struct Joiner {  // joins the started threads on every exit, so none is destroyed while joinable
+        std::vector<std::thread> th;
+        ~Joiner() {
+          for (auto& x : th)
+            if (x.joinable()) x.join();
+        }
+      } j;
+      std::vector<uint8_t> inline_pack(live.size(), 0);
       for (size_t q = 0; q < live.size(); q++) {
         const Shard& sh = parts[live[q]].call->shards[parts[live[q]].shard];
-        if (q == 0 || sh.set_end - sh.set_begin < 4096) pack(q);
+        inline_pack[q] = q == 0 || sh.set_end - sh.set_begin < 4096;
+        if (inline_pack[q]) continue;
+        try {
+          j.th.emplace_back(pack, q);
+        } catch (std::system_error&) {  // no thread: this part packs on the current one
+          inline_pack[q] = 1;
+        }
       }
-      for (auto& x : th) x.join();
+      for (size_t q = 0; q < live.size(); q++)
+        if (inline_pack[q]) pack(q);
     }
     blsgpu_batch mb{};
     mb.n_sets = n;
@@ -1897,6 +1914,13 @@ void create_streams(blsgpu_ctx* ctx, Device* d) {
     d->main_mask.assign((size_t)(n_cu + 31) / 32, 0);
     for (int i = 0; i < n_cu; i++) (i < part ? pmask : d->main_mask)[i / 32] |= 1u << (i % 32);
     if (!ctx->urgent_isolate) d->main_mask.clear();
+    // urgent_isolate 3 (diagnostics): the pipeline streams CU-masked with EVERY CU -- a masked stream's own costs
+    // (its own hardware queue, normal priority) without the partition
+    if (ctx->urgent_isolate == 3)
+      for (auto& w : d->main_mask) w = ~0u;
+    // urgent_isolate 2: the urgent streams stay unmasked at the highest priority (the partition is theirs because
+    // nothing else may run there, and an idle chip is theirs too)
+    if (ctx->urgent_isolate == 2) pmask.clear();
   }
   // The message branch (hash_to_G2 -> Miller lines -> Miller accumulation -> F reduction) is the serial chain that
   // bounds a device's throughput (~70% of the work, one in-order stream shared by the runs in flight): its stream
@@ -2283,7 +2307,8 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
       if (value < 0 || value > 128 || (value & 7)) return BLSGPU_ERR_ARGS;
       ctx->urgent_cus = value;
     } else {
-      ctx->urgent_isolate = value != 0;
+      if (value < 0 || value > 3) return BLSGPU_ERR_ARGS;
+      ctx->urgent_isolate = value;
     }
     return BLSGPU_OK;
   }

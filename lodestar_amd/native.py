@@ -87,6 +87,7 @@ class Stats(ctypes.Structure):
         ("fallback_jobs", ctypes.c_uint32),
         ("fallback_miller", ctypes.c_uint32),
         ("urgent_lane", ctypes.c_uint32),
+        ("host_ms", ctypes.c_double),
     ]
 
 

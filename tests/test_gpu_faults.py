@@ -276,3 +276,37 @@ def test_two_shards_c4_full_size_vs_oracle():
         assert (got != 1).sum() >= 100
     finally:
         c2.close()
+
+
+def test_eight_shards_c4_full_size_vs_oracle():
+    """C4's whole step through EIGHT in-process device contexts on device 0 (Context([0] * 8): eight dispatcher sets,
+    eight stream sets, eight table replicas -- the 8-GPU path of one process, on the one device this box has), with
+    route_split_sets 4096 so the 32,768-set call splits into 8 shards of 4,096: ~1% corrupted, job for job against the
+    oracle."""
+    from lodestar_amd.native import Context
+
+    c8 = Context([0] * 8)
+    try:
+        assert c8.device_count == 8
+        c8.set_option("route_split_sets", 4096)
+        signer = lambda sks, m: cpu.sign(sks, m, threads=THREADS)
+        w, n, desc, _ = bench.build_workload(c8, "C4", 0, 1, signer=signer)
+        assert n == 32768 and c8.pubkeys_count == 1 << 20
+        table = bench.oracle_table(w)
+        call = {k: v for k, v in w.items() if k != "expected" and not k.startswith("_")}
+        nmsg = len(w["_mkey"])
+        m2 = [bench.msg_j(k, 0xC48) for k in w["_mkey"]]
+        sg = cpu.sign(b"".join(w["_sk"]), b"".join(m2), threads=THREADS)
+        m2, buf, sl, _ = corrupt.corrupt_sets([sg[96 * i: 96 * i + 96] for i in range(nmsg)], m2,
+                                              np.random.default_rng(0xC48))
+        bad = dict(call, sigs=np.frombuffer(buf, np.uint8), sig_len=np.asarray(sl, np.uint32),
+                   msgs=np.frombuffer(b"".join(m2), np.uint8), sig_stride=192)
+        got, st = c8.verify_raw(**bad)
+        want, _ = cpu.verify_jobs(table=table, threads=THREADS, **bad)
+        assert st.devices_used == 8
+        assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+        assert (got != 1).sum() >= 100 and (got == 1).sum() > 30000
+        got, st = c8.verify_raw(**call)
+        assert st.devices_used == 8 and (got == 1).all()
+    finally:
+        c8.close()

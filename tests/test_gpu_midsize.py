@@ -189,3 +189,31 @@ def test_routing_whole_calls_and_split_epoch_calls(pool):
         assert all((g == 1).all() and st.devices_used == 1 for g, st in outs)
     finally:
         c2.close()
+
+
+def test_large_failing_jobs_fallback_vs_oracle(ctx, pool):
+    """Advisor r5: retried jobs of ~1k sets each in a small idle run (r_i sig_i formed speculatively) take the bucket
+    MSM and the wave-per-job reduce, not the one-lane reduce over thousands of sets.  Three 1,024-set block-shaped jobs
+    in one batch group (group_sets 4096), two of them with one set signed over another root, then 64 one-set jobs:
+    job for job equal to the oracle; the fallback re-checks the group's clean jobs."""
+    import time
+
+    sks, msgs, sigs, pks = pool
+    n = 3 * 1024 + 64
+    m = list(msgs[:n])
+    for bad in (100, 1024 + 700):  # jobs 0 and 1: one set over another root
+        m[bad] = msgs[N_MAX - 1 - bad]
+    sizes = [1024, 1024, 1024] + [1] * 64
+    call = dict(job_first_set=np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32), sigs=sigs[: 96 * n],
+                sig_len=np.full(n, 96, np.uint32), msgs=b"".join(m), pk_bytes=pks[: 96 * n],
+                job_flags=np.ones(len(sizes), np.uint8), sig_stride=96)
+    saved = ctx.get_option("group_sets")
+    ctx.set_option("group_sets", 4096)
+    try:
+        t0 = time.perf_counter()
+        got, st = compare(ctx, call)
+        print(f"two failing 1k-set jobs: {1e3 * (time.perf_counter() - t0):.1f} ms, fallback_jobs {st.fallback_jobs}")
+    finally:
+        ctx.set_option("group_sets", saved)
+    assert list(got[:3]) == [0, 0, 1] and (got[3:] == 1).all()
+    assert st.fallback_jobs >= 3
