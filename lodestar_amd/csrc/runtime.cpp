@@ -390,7 +390,7 @@ struct blsgpu_ctx {
   // urgent lane partition (set before the first call: the streams are created with it): CUs per device reserved for
   // the urgent streams, a multiple of 8; with urgent_isolate the pipeline streams are masked off them
   int64_t urgent_cus = 0;
-  int64_t urgent_isolate = 1;
+  int64_t urgent_isolate = 1;  // (no effect without a partition)
 };
 
 namespace {
@@ -1839,8 +1839,9 @@ void worker_loop(Device* d, Slot* sl) {
   }
 }
 
-// The urgent lane's dispatcher: takes urgent calls one at a time, oldest first, and runs each on the lane's own stream
-// pairs (run_shard: Slot::urgent) -- the reference's verifyOnMainThread verifies at once, outside the pool queue
+// The urgent lane's dispatcher: takes the oldest urgent call and the compatible urgent calls queued behind it (up to
+// urgent_max_sets sets: a burst of urgent calls becomes one run, not a queue of runs), and runs them on the lane's own
+// stream pairs (run_shard: Slot::urgent) -- the reference's verifyOnMainThread verifies at once, outside the pool queue
 // (multithread/index.ts:138-151).  `alone` holds for its streams, so a run takes the latency forms of an idle device:
 // the speculative MSM and the pubkey branch on the idle pair, r_i sig_i beside the batch pass, cooperative fallback
 // checks.  Exits when the device stops and its urgent queue is drained.
@@ -1848,19 +1849,51 @@ void urgent_loop(Device* d, Slot* sl) {
   tl_dispatcher = true;
   (void)hipSetDevice(d->id);
   for (;;) {
-    Task t;
+    std::vector<Task> parts;
     {
       std::unique_lock<std::mutex> lk(d->q_mu);
       d->q_cv.wait(lk, [&] { return d->stop || !d->uqueue.empty(); });
       if (d->uqueue.empty()) return;  // stop requested and nothing left
-      t = d->uqueue.front();
+      parts.push_back(d->uqueue.front());
       d->uqueue.pop_front();
+      const Call* c0 = parts[0].call;
+      uint32_t total = task_sets(parts[0]);
+      while (!d->uqueue.empty()) {
+        const Task& nx = d->uqueue.front();
+        if ((int64_t)(total + task_sets(nx)) > c0->opt.urgent_max_sets || pk_mode(nx.call->b) != pk_mode(c0->b) ||
+            !nx.call->opt.same_run(c0->opt))
+          break;
+        total += task_sets(nx);
+        parts.push_back(nx);
+        d->uqueue.pop_front();
+      }
     }
     sl->alone = true;
     tl_run_t0 = std::chrono::steady_clock::now();
     tl_merge_ms = 0;
-    run_task(*d, *sl, t);  // completes the call (it has one shard)
-    d->upending.fetch_sub(1, std::memory_order_relaxed);
+    const size_t np = parts.size();
+    if (np == 1) {
+      run_task(*d, *sl, parts[0]);  // completes the call
+    } else {
+      std::vector<int> rcs(np, BLSGPU_OK);
+      try {
+        std::shared_lock<std::shared_mutex> tl(d->table_mu);
+        run_merged(*d, *sl, parts, rcs);
+      } catch (...) {  // run_merged catches its own failures; this only guards the lock
+        for (size_t p = 0; p < np; p++) {
+          const Shard& sh = parts[p].call->shards[parts[p].shard];
+          for (uint32_t j = sh.job_begin; j < sh.job_end; j++) parts[p].call->job_result[j] = -BLSGPU_DEVICE_ERROR;
+          rcs[p] = BLSGPU_DEVICE_ERROR;
+        }
+      }
+      for (size_t p = 0; p < np; p++) {
+        Call* c = parts[p].call;
+        c->rc[parts[p].shard] = rcs[p];
+        c->sst[parts[p].shard].urgent_lane = 1;
+        if (c->remaining.fetch_sub(1) == 1) finish_call(c);
+      }
+    }
+    d->upending.fetch_sub((int)np, std::memory_order_relaxed);
   }
 }
 
@@ -1892,13 +1925,17 @@ hipStream_t make_stream(const std::vector<uint32_t>& mask, int prio) {
 }
 
 // The device's pipeline streams and its urgent lane's (created with the first call, so "urgent_cus" set after init
-// applies).  The urgent partition is CU mask bits [0, urgent_cus): the driver deals mask bits round-robin over the
-// XCDs (bit i -> XCD i % 8 in SPX mode; measured, profiles/r06_cu_probe.json), so a multiple of 8 bits gives every XCD
-// the same number of partition CUs -- a workgroup is dealt to any XCD, and an XCD without a CU of the stream's mask
-// would never run it.  With isolation the pipeline streams (and the slots' fallback streams) are masked to the
-// complement: the partition then always has free SIMDs for an urgent run, at the cost of those CUs' throughput and of
-// the pipeline streams' priorities (a CU-masked stream has normal priority).  Without a partition the urgent streams
-// take the device's highest priority.
+// applies).  The urgent streams are CU-masked streams (hipExtStreamCreateWithCUMask), which HIP gives hardware queues
+// of their own: an urgent kernel never waits in a queue behind a pipeline kernel, only for free SIMDs.  Their mask is
+// every CU, or with "urgent_cus" > 0 a partition, mask bits [0, urgent_cus): the driver deals mask bits round-robin
+// over the XCDs (bit i -> XCD i % 8 in SPX mode, then over each XCD's shader engines; profiles/r06_cu_probe.json), so a
+// multiple of 8 bits gives every XCD the same number of partition CUs -- a workgroup is dealt to any XCD, and an XCD
+// without a CU of the stream's mask would never run it.  With urgent_isolate 1 the pipeline streams (and the slots'
+// fallback streams) are masked to the complement, so the partition always has free SIMDs for an urgent run.  Measured
+// (profiles/r06_urgent_ab.json): that costs ~10% of C2 throughput for 8 CUs, not 3% -- the partition leaves shader
+// engine 0 of every XCD with 7 of its 8 CUs, the dispatcher deals workgroups evenly over the engines, and that engine
+// finishes last -- so the default is no partition.  urgent_isolate 2: plain highest-priority urgent streams (HIP deals
+// them over its shared hardware queues); 3 (diagnostics): the pipeline streams masked with every CU.
 void create_streams(blsgpu_ctx* ctx, Device* d) {
   HIPCHK(hipSetDevice(d->id));
   int prio_lo = 0, prio_hi = 0;
@@ -1907,21 +1944,17 @@ void create_streams(blsgpu_ctx* ctx, Device* d) {
   HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, d->id));
   const int part = (int)std::min<int64_t>(ctx->urgent_cus, n_cu / 2) & ~7;
   d->urgent_cus = part;
-  std::vector<uint32_t> pmask;
+  const size_t words = (size_t)(n_cu + 31) / 32;
+  std::vector<uint32_t> pmask(words, 0);
   d->main_mask.clear();
-  if (part > 0) {
-    pmask.assign((size_t)(n_cu + 31) / 32, 0);
-    d->main_mask.assign((size_t)(n_cu + 31) / 32, 0);
-    for (int i = 0; i < n_cu; i++) (i < part ? pmask : d->main_mask)[i / 32] |= 1u << (i % 32);
-    if (!ctx->urgent_isolate) d->main_mask.clear();
-    // urgent_isolate 3 (diagnostics): the pipeline streams CU-masked with EVERY CU -- a masked stream's own costs
-    // (its own hardware queue, normal priority) without the partition
-    if (ctx->urgent_isolate == 3)
-      for (auto& w : d->main_mask) w = ~0u;
-    // urgent_isolate 2: the urgent streams stay unmasked at the highest priority (the partition is theirs because
-    // nothing else may run there, and an idle chip is theirs too)
-    if (ctx->urgent_isolate == 2) pmask.clear();
+  for (int i = 0; i < n_cu; i++)
+    if (part == 0 || i < part) pmask[i / 32] |= 1u << (i % 32);
+  if (part > 0 && ctx->urgent_isolate == 1) {
+    d->main_mask.assign(words, 0);
+    for (int i = part; i < n_cu; i++) d->main_mask[i / 32] |= 1u << (i % 32);
   }
+  if (ctx->urgent_isolate == 3) d->main_mask.assign(words, ~0u);
+  if (ctx->urgent_isolate == 2) pmask.clear();
   // The message branch (hash_to_G2 -> Miller lines -> Miller accumulation -> F reduction) is the serial chain that
   // bounds a device's throughput (~70% of the work, one in-order stream shared by the runs in flight): its stream
   // gets the device's highest priority, so its kernels take free SIMDs first and the signature / pubkey branches

@@ -86,6 +86,9 @@ class BlsGpuVerifier {
     // 1 = the pool's job / request / chunk structure (batchRetries / batchSigsSuccess in the reference's units)
     if (opts.groupPolicy) addon.setOption(this.ctx, "group_policy", opts.groupPolicy);
     this.seed = opts.seed || 0; // 0 = OS CSPRNG batch scalars; fixed only for comparison runs
+    // verifyOnMainThread calls are latency-critical exceptions to the pool (the block proposer signature): they run on
+    // the device's urgent lane.  The single-thread verifier sends every call that way and keeps the shared pipeline.
+    this.urgentMainThread = true;
     this.metrics = modules.metrics || null;
     this.closed = false;
     this.bufferedJobs = null; // {jobs, sigCount, timeout}
@@ -261,7 +264,7 @@ class BlsGpuVerifier {
       jobFirstSet[ji] = i;
       // BLSGPU_JOB_BATCHABLE, and BLSGPU_JOB_URGENT for verifyOnMainThread jobs: the runtime runs those on the
       // device's urgent lane, never queued behind or merged with the gossip flood (multithread/index.ts:138-151)
-      jobFlags[ji] = (j.batchable ? JOB_BATCHABLE : 0) | (j.mainThread ? JOB_URGENT : 0);
+      jobFlags[ji] = (j.batchable ? JOB_BATCHABLE : 0) | (j.mainThread && this.urgentMainThread ? JOB_URGENT : 0);
       if (m && m.jobWaitTime && j.addedTimeMs) m.jobWaitTime.observe((now - j.addedTimeMs) / 1000);
       for (const s of j.sets) {
         msgs.set(s.msg.subarray(0, 32), 32 * i);
@@ -335,6 +338,13 @@ class BlsGpuVerifier {
  * errors reject.  Same device path: one non-batchable job per call.
  */
 class BlsGpuSingleThreadVerifier extends BlsGpuVerifier {
+  constructor(opts = {}, modules = {}) {
+    super(opts, modules);
+    // every call is "main thread" here, so none is an exception: calls share the device pipeline (no urgent lane, which
+    // runs one burst of calls at a time)
+    this.urgentMainThread = false;
+  }
+
   async verifySignatureSets(sets) {
     if (sets.length === 0) throw new Error("Empty signature set");
     return super.verifySignatureSets(sets, {verifyOnMainThread: true});

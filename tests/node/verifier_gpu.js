@@ -236,6 +236,7 @@ async function main() {
   const each = fx.cases.find((c) => c.name === "each_alone/plain");
   const so = await Promise.all(each.jobs.map((j) => settle(st.verifySignatureSets(j.map((k) => toSet(fx.sets[k], true))))));
   so.forEach((o, ji) => expectOutcome(o, each.expected[ji], `single-thread job ${ji}`, true));
+  assert.ok(!st.stats.urgentCalls, "the single-thread verifier's calls share the pipeline, not the urgent lane");
   const se = await settle(st.verifySignatureSets([]));
   assert.ok(se.error && se.error.message === "Empty signature set");
   for (const n of ["totalJobsStarted", "totalSigSetsStarted", "jobsWorkerTime", "timePerSigSet", "jobWaitTime",
