@@ -41,11 +41,16 @@ def tu_defines():
     return out
 
 
-# Per-TU compiler flags.  The hash and pubkey stages schedule for ILP (LLVM's max-ILP strategy): their kernels run one
-# wave per SIMD, so occupancy-driven scheduling buys nothing there (C2 +1.5% at 20 steps, +1.7% at 100; the same
-# strategy on every TU lost 6%: the Miller accumulation and the decode spill more under it).
+# Per-TU compiler flags.  The pubkey stage schedules for ILP (LLVM's max-ILP strategy): its kernels run one wave per
+# SIMD, so occupancy-driven scheduling buys nothing there (round 4: hash + pubkey TUs C2 +1.5% at 20 steps, +1.7% at
+# 100; the same strategy on every TU lost 6%: the Miller accumulation and the decode spill more under it).  Round 6:
+# the hash TUs' kernels now run two waves per SIMD (lane pairs), where max-ILP only raises register pressure: the
+# cofactor clearing (k_hash.hip) schedules for minimum registers (k_hash_clear2 713 -> 366 spilled VGPRs, 848 -> 496 B
+# of scratch per lane) and the maps (k_hmap.hip) with the default scheduler (k_hash_map 214 -> 98, 1,984 -> 1,664 B);
+# C2 equal within noise (3.40M vs 3.39M at 20 steps, 3.83M vs 3.84M at 100; profiles/r06_hash_sched_ab.json).
 _ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-TU_CFLAGS = {"k_hash.hip": _ILP, "k_hmap.hip": _ILP, "k_pk.hip": _ILP}
+_MINREG = ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]
+TU_CFLAGS = {"k_hash.hip": _MINREG, "k_pk.hip": _ILP}
 
 
 def tu_cflags():

@@ -85,15 +85,11 @@ def test_urgent_calls_alone_vs_oracle(env):
         assert st.urgent_lane == 1
 
 
-def test_urgent_calls_overtake_a_gossip_flood(env):
-    """FLOOD_CALLS x 16,384-set calls (two merged pipeline runs of 131,072 sets) are queued first; the urgent calls,
-    submitted together behind them, complete before the flood's median call, and every one gives the oracle's
-    answer."""
-    ctx, sks, pks, flood = env
-    calls = [urgent_call(sks, idx, kinds, 100 + t) for t, (idx, kinds, _) in enumerate(URGENT_CASES)]
-    wants = [oracle_result(pks, c, bench.SEED + 100 + t) for t, c in enumerate(calls)]
-    done = [None] * FLOOD_CALLS
-    errs = []
+def run_behind_flood(ctx, flood, calls, seeds, twin=None):
+    """Queues the flood (FLOOD_CALLS threads), then after 30 ms submits the urgent calls together (and, with `twin`, the
+    same calls without the urgent flag, as ordinary calls queued behind the flood).  Returns (urgent outcomes [(result,
+    lane, ms, done_t)], twin outcomes, sorted flood completion times (ms from the flood's submission))."""
+    done, errs = [None] * FLOOD_CALLS, []
 
     def flood_call(k):
         try:
@@ -104,34 +100,68 @@ def test_urgent_calls_overtake_a_gossip_flood(env):
             errs.append(repr(e))
         done[k] = time.perf_counter()
 
+    def one(c, seed, out, t):
+        t1 = time.perf_counter()
+        got, st = ctx.verify_raw(**c, seed=seed)
+        out[t] = (int(got[0]), int(st.urgent_lane), (time.perf_counter() - t1) * 1e3, time.perf_counter())
+
     th = [threading.Thread(target=flood_call, args=(k,)) for k in range(FLOOD_CALLS)]
     t0 = time.perf_counter()
     for x in th:
         x.start()
     time.sleep(0.03)  # the flood is queued on the device
-    outs = [None] * len(calls)
-
-    def urgent(t):
-        t1 = time.perf_counter()
-        got, st = ctx.verify_raw(**calls[t], seed=bench.SEED + 100 + t)
-        outs[t] = (int(got[0]), int(st.urgent_lane), (time.perf_counter() - t1) * 1e3, time.perf_counter())
-
-    uth = [threading.Thread(target=urgent, args=(t,)) for t in range(len(calls))]
+    outs, touts = [None] * len(calls), [None] * len(calls)
+    uth = [threading.Thread(target=one, args=(c, seeds[t], outs, t)) for t, c in enumerate(calls)]
+    if twin:
+        uth += [threading.Thread(target=one, args=(dict(c, job_flags=np.zeros(1, np.uint8)), seeds[t], touts, t))
+                for t, c in enumerate(calls)]
     for x in uth:
         x.start()
-    for x in uth:
-        x.join(timeout=120)
-    for x in th:
+    for x in uth + th:
         x.join(timeout=120)
     assert not errs, errs
-    flood_ms = sorted((d - t0) * 1e3 for d in done)
-    u_done = max((o[3] - t0) * 1e3 for o in outs)
-    print(f"urgent latencies behind the flood (ms): {[round(o[2], 2) for o in outs]}; flood done at {flood_ms[0]:.1f} "
-          f".. {flood_ms[-1]:.1f} ms; urgent calls done at {u_done:.1f} ms")
-    for t, o in enumerate(outs):
-        assert o[0] == wants[t], (t, o, wants[t])
-        assert o[1] == 1
-    assert u_done < flood_ms[FLOOD_CALLS // 2], "urgent calls did not overtake the flood"
+    rel = lambda o: [(r, lane, ms, (d - t0) * 1e3) for r, lane, ms, d in o] if o[0] else None
+    return rel(outs), rel(touts) if twin else None, sorted((d - t0) * 1e3 for d in done)
+
+
+@pytest.mark.parametrize("lane", ["default", "partition"])
+def test_urgent_calls_overtake_a_gossip_flood(env, lane):
+    """FLOOD_CALLS x 16,384-set calls (two merged pipeline runs of 131,072 sets) are queued first, then the urgent calls
+    (valid, wrong message, malformed signature, 3-set jobs), submitted together: every one gives the oracle's answer on
+    the urgent lane.  Default lane (no CU partition): the urgent calls finish before the same calls submitted as
+    ordinary calls behind the flood (those wait for the queue).  With an isolated 8-CU partition (urgent_cus 8): they
+    finish before the flood's median call."""
+    ctx0, sks, pks, flood = env
+    ctx = ctx0
+    if lane == "partition":
+        from lodestar_amd.native import Context
+
+        ctx = Context([0])
+        ctx.set_option("urgent_cus", 8)
+        ctx.set_option("urgent_isolate", 1)
+        ctx.upload_pubkeys(0, pks)
+    try:
+        calls = [urgent_call(sks, idx, kinds, 100 + t) for t, (idx, kinds, _) in enumerate(URGENT_CASES)]
+        seeds = [bench.SEED + 100 + t for t in range(len(calls))]
+        wants = [oracle_result(pks, c, s) for c, s in zip(calls, seeds)]
+        ctx.verify_raw(**calls[0], seed=seeds[0])  # the lane's buffers exist before timing
+        outs, touts, flood_ms = run_behind_flood(ctx, flood, calls, seeds, twin=lane == "default")
+        u_done = max(o[3] for o in outs)
+        print(f"[{lane}] urgent latencies behind the flood (ms): {[round(o[2], 2) for o in outs]}, done at "
+              f"{u_done:.1f} ms; flood done at {flood_ms[0]:.1f} .. {flood_ms[-1]:.1f} ms"
+              + (f"; the same calls queued as ordinary calls done at {max(o[3] for o in touts):.1f} ms" if touts else ""))
+        for t, o in enumerate(outs):
+            assert o[0] == wants[t], (t, o, wants[t])
+            assert o[1] == 1
+        if touts:
+            for t, o in enumerate(touts):
+                assert o[0] == wants[t] and o[1] == 0
+            assert u_done < min(o[3] for o in touts), "urgent calls did not overtake the queue"
+        else:
+            assert u_done < flood_ms[FLOOD_CALLS // 2], "urgent calls did not overtake the flood"
+    finally:
+        if ctx is not ctx0:
+            ctx.close()
 
 
 def test_large_urgent_call_takes_the_queue_head(env):

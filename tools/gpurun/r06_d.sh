@@ -1,6 +1,6 @@
 # usage: bash tools/gpurun/r06_d.sh TAG -- urgent lane on dedicated CU-masked queues: the urgent tests; urgent latency
 # under a 200-step C2 flood (default lane, plain high-priority streams, the isolated 8-CU partition); the driver's
-# command x3; a kernel trace of isolated urgent calls; then the whole GPU suite
+# command x3; a kernel trace of isolated urgent calls; the whole GPU suite; the hash-TU scheduler variants (r06_f.sh)
 set -e
 TAG=$1
 cd $GRAFT_REPO_ROOT
@@ -24,6 +24,7 @@ timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_RO
   -- python3 $GRAFT_REPO_ROOT/tools/urgent_latency.py --reps 10 > $GRAFT_REPO_ROOT/gpurun_out/${TAG}_utrace.log 2>&1
 cd $GRAFT_REPO_ROOT
 rc=0
-timeout -k 10 1500 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
   > gpurun_out/${TAG}_gpu_tests.log 2>&1 || rc=$?
-exit $rc
+[ $rc -le 1 ] || exit $rc
+bash tools/gpurun/r06_f.sh ${TAG}v base noilp mix

@@ -1,0 +1,13 @@
+# usage: bash tools/gpurun/r06_h.sh TAG -- the candidate library (hash TUs re-scheduled): the whole GPU suite (the urgent
+# flood test with its default-lane and partition forms), smoke, then three interleaved rounds of spec_large on / off
+# on C5, C1 and C4 (r06_e.sh)
+set -e
+TAG=$1
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+rc=0
+timeout -k 10 600 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread \
+  > gpurun_out/${TAG}_gpu_tests.log 2>&1 || rc=$?
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.log 2>&1
+bash tools/gpurun/r06_e.sh ${TAG}s
