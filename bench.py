@@ -315,7 +315,7 @@ def roofline(runs, n_sets, group_count, pubkeys_per_set, sets_per_s, miller_k=2,
     return out
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r06_pmc_traffic.json")
 # grid work-items per distinct message (C2: one message per set) of the hash stage's launches; k_batch_inv runs one
 # lane per INV_K = 16 elements (csrc/k_inv.hip) and twice per stage (before the maps, before the affine conversion),
 # k_hash_map two lanes per message (one SSWU map each), k_hash_clear2 a lane pair per message

@@ -1,6 +1,5 @@
-# usage: bash tools/gpurun/r06_h.sh TAG -- the candidate library (hash TUs re-scheduled): the whole GPU suite (the urgent
-# flood test with its default-lane and partition forms), smoke, then three interleaved rounds of spec_large on / off
-# on C5, C1 and C4 (r06_e.sh)
+# usage: bash tools/gpurun/r06_h.sh TAG -- the candidate library: the whole GPU suite and smoke, then the round-6
+# evidence (r06_final.sh)
 set -e
 TAG=$1
 cd $GRAFT_REPO_ROOT
@@ -10,4 +9,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout
   > gpurun_out/${TAG}_gpu_tests.log 2>&1 || rc=$?
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.log 2>&1
-bash tools/gpurun/r06_e.sh ${TAG}s
+bash tools/gpurun/r06_final.sh ${TAG}f
