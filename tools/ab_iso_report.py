@@ -1,4 +1,4 @@
-"""Summary of an A/B run of tools/gpurun/r04_iso_ab.sh: per variant, the isolation-profile stage table
+"""Summary of an A/B run of a round-4 isolation A/B script (git history: tools/gpurun/r04_iso_ab.sh): per variant, the isolation-profile stage table
 (tools/iso_table.py) and the 20-step C2 bench value.  Tooling only.
     python tools/ab_iso_report.py TAG SETS variant ..."""
 import contextlib

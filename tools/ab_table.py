@@ -1,4 +1,4 @@
-"""Summarises interleaved A/B bench lines (tools/gpurun/r03_ab.sh): per variant, value / hash-stage frac /
+"""Summarises interleaved A/B bench lines (tools/gpurun/r06_f.sh and earlier A/B scripts): per variant, value / hash-stage frac /
 isolated stage times / p50.   python tools/ab_table.py gpurun_out/TAG"""
 import glob
 import json

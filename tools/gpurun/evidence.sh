@@ -1,4 +1,4 @@
-# usage: bash tools/gpurun/r05_evidence.sh TAG -- evidence of the driver's command (C2, 20 steps, 5 warmup) on the
+# usage: bash tools/gpurun/evidence.sh TAG -- evidence of the driver's command (C2, 20 steps, 5 warmup) on the
 # current build: kernel trace + stats, FETCH_SIZE / WRITE_SIZE PMC passes, SQ counter pass (each its own run, kernel
 # trace only, the program directly after --)
 set -e

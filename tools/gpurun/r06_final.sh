@@ -9,7 +9,7 @@ TAG=$1
 R=$GRAFT_REPO_ROOT
 cd $R
 mkdir -p gpurun_out
-bash tools/gpurun/r05_evidence.sh ${TAG}e
+bash tools/gpurun/evidence.sh ${TAG}e
 cd $R
 python tools/pmc_to_json.py gpurun_out/${TAG}e profiles/r06_pmc_traffic.json > gpurun_out/${TAG}_pmc_fold.log 2>&1
 cp profiles/r06_pmc_traffic.json gpurun_out/${TAG}_pmc_traffic.json

@@ -1,4 +1,4 @@
-"""Per-kernel efficiency in an isolation profile (tools/gpurun/r04_iso.sh: one C2 call of N sets per step, every
+"""Per-kernel efficiency in an isolation profile (round-4 script in git history, tools/gpurun/r04_iso.sh: one C2 call of N sets per step, every
 branch on one stream, so each kernel runs alone on the chip): average launch time, the stage's algorithmic
 Montgomery multiplications (lodestar_amd/op_counts.json) and the fraction of the chip's measured Montgomery-product
 rate (29.17e12 v_mad_u64_u32 lane-ops/s / 392 MADs per 14-limb product = 7.44e10 products/s).  Tooling only.

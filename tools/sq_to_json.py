@@ -1,4 +1,4 @@
-"""Folds a rocprofv3 SQ/GRBM PMC pass of the driver's command (tools/gpurun/r04_sq.sh) into a per-kernel VALU table:
+"""Folds a rocprofv3 SQ/GRBM PMC pass of the driver's command (tools/gpurun/evidence.sh) into a per-kernel VALU table:
 
   * wave_cycles        SQ_WAVE_CYCLES summed over the kernel's dispatches (wave-resident cycles, per XCD sums added)
   * frac_active_valu   SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: the fraction of a resident wave's cycles in which it was

@@ -1,4 +1,4 @@
-"""Prints the bench lines of a gpurun sweep log (tools/gpurun/r02_sweep2.sh / r02_sweep3.sh) as a table."""
+"""Prints the bench lines of a gpurun sweep log (tools/gpurun/sweep.sh) as a table."""
 import json
 import sys
 

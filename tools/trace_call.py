@@ -1,4 +1,4 @@
-"""Timeline of one call of a serial kernel trace (tools/gpurun/r03_lat.sh): kernels from the N-th-last k_hash_prep to
+"""Timeline of one call of a serial kernel trace (e.g. rocprofv3 --kernel-trace of tools/urgent_latency.py): kernels from the N-th-last k_hash_prep to
 the next, with queue, start / end (us from the call's first kernel) and duration.
     python tools/trace_call.py gpurun_out/TAG/run_kernel_trace.csv [N]"""
 import csv
