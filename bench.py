@@ -324,7 +324,7 @@ PMC_ITEMS_PER_UNIT = {"k_hash_map": 2.0, "k_hash_clear2": 2.0, "k_batch_inv": 2.
 
 def pmc_traffic(kernel, n_sets):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes over the driver's own command
-    (tools/gpurun/r03_e.sh; FETCH_SIZE doubled for the gfx950 half-count of wide reads, WRITE_SIZE as is;
+    (tools/gpurun/evidence.sh; FETCH_SIZE doubled for the gfx950 half-count of wide reads, WRITE_SIZE as is;
     MI355X_MICROARCH.md HBM section), kept as bytes per grid work-item because the merged runs differ in size, and
     multiplied by the work-items of an n_sets launch; None when no PMC file is committed."""
     if not n_sets or not os.path.exists(PMC_FILE):
@@ -384,8 +384,14 @@ def host_cpus():
         pass
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     threads = min(len(aff), share) if share > 0 else len(aff)
+    quota = None  # the cgroup's CPU bandwidth limit (cgroup v2 cpu.max "quota period"), in CPUs
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        pass
     return {"threads": max(1, threads), "affinity_cpus": len(aff), "affinity_physical_cores": len(phys) or None,
-            "cpu_share_env": share or None, "os_cpu_count": os.cpu_count(), "model": model}
+            "cpu_share_env": share or None, "cgroup_cpu_quota": quota, "os_cpu_count": os.cpu_count(), "model": model}
 
 
 def oracle_table(work):
@@ -430,7 +436,8 @@ def cpu_baseline_all_cores(calls, expected, table, hc):
     return {"value": round(k * n_sets / dt, 2), "unit": "sets/s", "cores": threads, "kind": "port",
             "sample": f"{k} in-flight steps ({k * n_sets} sets, {st.work_requests} worker requests) through "
                       f"oracle/blscpu.c on all {threads} CPUs of the affinity mask "
-                      f"({hc['affinity_physical_cores']} physical cores), {dt:.2f} s, results "
+                      f"({hc['affinity_physical_cores']} physical cores; cgroup CPU quota "
+                      f"{hc['cgroup_cpu_quota'] or 'none'}), {dt:.2f} s, results "
                       f"{'identical to' if agree else 'DIFFERENT from'} the GPU's",
             "results_match_gpu": agree,
             "blst_anchor_sets_per_s": BLST_SETS_PER_CORE * (hc["affinity_physical_cores"] or threads)}
@@ -456,7 +463,8 @@ def cpu_baseline(call, expected, table, hc):
                       f"batch chunks of >= 16 jobs) through oracle/blscpu.c on {threads} threads of '{hc['model']}', "
                       f"{dt:.2f} s, results {'identical to' if agree else 'DIFFERENT from'} the GPU's",
             "results_match_gpu": agree,
-            "host": {k: hc[k] for k in ("affinity_cpus", "affinity_physical_cores", "cpu_share_env", "os_cpu_count")},
+            "host": {k: hc[k] for k in ("affinity_cpus", "affinity_physical_cores", "cpu_share_env", "cgroup_cpu_quota",
+                                        "os_cpu_count")},
             "blst_anchor_sets_per_s": BLST_SETS_PER_CORE * threads,
             "blst_anchor_sets_per_s_affinity_cores": BLST_SETS_PER_CORE * cores,
             "blst_anchor": f"{BLST_SETS_PER_CORE:.0f} sets/s/core (reference lodestar.ts:454 ~0.9 ms/set/thread, "

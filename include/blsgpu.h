@@ -198,12 +198,14 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * stream),
  * "urgent_lane" (calls with a BLSGPU_JOB_URGENT job run on the device's urgent lane, 0/1, default 1), "urgent_max_sets"
  * (larger urgent calls are queued at the head of the device queue instead, default 512), "urgent_excl" (urgent runs
- * may use the exclusive-CU padding of the cooperative kernels, 0/1, default 0), "urgent_cus" (CUs per device reserved
+ * may use the exclusive-CU padding of the cooperative kernels, 0/1, default 0), "urgent_wait_us" (the urgent dispatcher
+ * lingers this long after an urgent call for more of a burst, merged into one run, default 300), "urgent_cus" (CUs per device reserved
  * for the urgent lane's streams, a multiple of 8 up to 128, 0 = no partition: the lane's streams take the highest
  * priority; CU mask bits [0, urgent_cus), which the driver deals round-robin over the XCDs) and "urgent_isolate" (with a
  * partition, the pipeline streams are masked off it; 2: and the urgent streams are left unmasked at the highest
  * priority, so an idle chip is theirs too; 3, diagnostics: the pipeline streams masked with every CU; 0..3) -- these two only before the first call (the
- * streams are created with it; BLSGPU_ERR_ARGS afterwards),
+ * streams are created with it; BLSGPU_ERR_ARGS afterwards), "blocking_sync" (the dispatcher threads block on their
+ * runs' completion events instead of spinning, 0/1, default 1; before the first call only),
  * "lane_tail_min" / "lane_tail_parts" (runs of >= lane_tail_min sets take lane forms of the Horner passes (bit 0)
  * and of MillerLoop(-g1, S) (bit 1) instead of the cooperative workgroups; default 0 = never, parts 3), "serial"
  * (diagnostics: every branch of a run on one stream, so each kernel runs alone on the chip; 0/1, default 0), "profile" (per-stage kernel times in

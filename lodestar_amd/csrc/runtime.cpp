@@ -203,6 +203,7 @@ struct Device {
   std::atomic<int> upending{0};  // urgent calls queued or running here (routing of urgent calls)
   int urgent_cus = 0;            // CUs of the partition the streams were created with (0 = none)
   std::vector<uint32_t> main_mask;  // CU mask of the pipeline and fallback streams (empty = all CUs, priorities)
+  bool blocking_sync = true;        // the dispatchers' wait events block instead of spinning (create_slot_events)
 };
 
 // Device-failure injection (blsgpu_debug_inject, tests only): the next `count` pipeline runs after `skip` more fail as
@@ -252,6 +253,7 @@ struct Options {  // snapshot taken at the start of each call
   int64_t urgent_lane = 1;        // calls with a BLSGPU_JOB_URGENT job run on the device's urgent lane
   int64_t urgent_max_sets = 512;  // larger urgent calls go to the head of the device queue instead
   int64_t urgent_excl = 0;        // urgent runs may use the exclusive-CU padding of the cooperative kernels
+  int64_t urgent_wait_us = 300;   // the urgent dispatcher lingers this long for more urgent calls of a burst
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
            group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&
@@ -391,6 +393,7 @@ struct blsgpu_ctx {
   // the urgent streams, a multiple of 8; with urgent_isolate the pipeline streams are masked off them
   int64_t urgent_cus = 0;
   int64_t urgent_isolate = 1;  // (no effect without a partition)
+  int64_t blocking_sync = 1;   // dispatchers block on their runs' completion events instead of spinning
 };
 
 namespace {
@@ -1858,6 +1861,11 @@ void urgent_loop(Device* d, Slot* sl) {
       d->uqueue.pop_front();
       const Call* c0 = parts[0].call;
       uint32_t total = task_sets(parts[0]);
+      // a burst of urgent calls (several main-thread verifications issued in one JS tick) arrives within microseconds:
+      // linger up to urgent_wait_us so it becomes one run instead of a run and a queue behind it
+      if (c0->opt.urgent_wait_us > 0 && d->uqueue.empty() && !d->stop)
+        d->q_cv.wait_for(lk, std::chrono::microseconds(c0->opt.urgent_wait_us),
+                         [&] { return d->stop || !d->uqueue.empty(); });
       while (!d->uqueue.empty()) {
         const Task& nx = d->uqueue.front();
         if ((int64_t)(total + task_sets(nx)) > c0->opt.urgent_max_sets || pk_mode(nx.call->b) != pk_mode(c0->b) ||
@@ -1971,15 +1979,23 @@ void create_streams(blsgpu_ctx* ctx, Device* d) {
   for (int k = 0; k < 4; k++) d->ust[k] = make_stream(pmask, prio_hi);
 }
 
+// A slot's events: the two its dispatcher waits on (join_msg, done) block the thread in the driver when
+// d->blocking_sync is set (hipEventBlockingSync) instead of spinning -- a dispatcher waits ~10-40 ms per run, and three
+// spinning per device cost ~1 host core per million sets/s (round 6, bench.py "host").
+void create_slot_events(Device* d, Slot* s) {
+  const unsigned wait_flags = hipEventDisableTiming | (d->blocking_sync ? hipEventBlockingSync : 0u);
+  for (hipEvent_t* e : {&s->join_in, &s->join_pk, &s->join_mask, &s->join_gsm, &s->join_dec, &s->join_msm, &s->join_rsig})
+    HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  for (hipEvent_t* e : {&s->join_msg, &s->done}) HIPCHK(hipEventCreateWithFlags(e, wait_flags));
+  for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
+}
+
 void add_slot(Device* d) {  // caller holds d->q_mu (or the device is not yet shared)
   Slot* s = new Slot();
   HIPCHK(hipSetDevice(d->id));
   try {
     s->set_stream(d->st[kSig]);
-    for (hipEvent_t* e : {&s->join_in, &s->join_msg, &s->join_pk, &s->join_mask, &s->join_gsm, &s->join_dec, &s->join_msm,
-                          &s->join_rsig, &s->done})
-      HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
+    create_slot_events(d, s);
     int prio_lo = 0, prio_hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     s->fb = make_stream(d->main_mask, prio_lo);
@@ -2061,17 +2077,17 @@ int ensure_slots(blsgpu_ctx* ctx) {
   if (ctx->slots_started) return BLSGPU_OK;
   try {
     for (Device* d : ctx->devs) {
-      if (!d->st[0]) create_streams(ctx, d);
+      if (!d->st[0]) {
+        d->blocking_sync = ctx->blocking_sync != 0;
+        create_streams(ctx, d);
+      }
       resize_slots(d, ctx->slots_per_device);
       if (!d->uslot) {  // the urgent lane: one slot, its own dispatcher
         Slot* u = new Slot();
         u->urgent = true;
         try {
           u->set_stream(d->ust[0]);
-          for (hipEvent_t* e : {&u->join_in, &u->join_msg, &u->join_pk, &u->join_mask, &u->join_gsm, &u->join_dec,
-                                &u->join_msm, &u->join_rsig, &u->done})
-            HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-          for (auto& e : u->ev) HIPCHK(hipEventCreate(&e));
+          create_slot_events(d, u);
         } catch (HipError&) {
           free_slot(d, u);
           throw;
@@ -2333,10 +2349,13 @@ int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* 
 int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return BLSGPU_ERR_ARGS;
   std::string k(key);
-  if (k == "urgent_cus" || k == "urgent_isolate") {  // stream creation: before the first call only
+  if (k == "urgent_cus" || k == "urgent_isolate" || k == "blocking_sync") {  // stream / event creation: first call
     std::lock_guard<std::mutex> sk(ctx->slots_mu);
     if (ctx->slots_started) return BLSGPU_ERR_ARGS;
-    if (k == "urgent_cus") {
+    if (k == "blocking_sync") {
+      if (value < 0 || value > 1) return BLSGPU_ERR_ARGS;
+      ctx->blocking_sync = value;
+    } else if (k == "urgent_cus") {
       if (value < 0 || value > 128 || (value & 7)) return BLSGPU_ERR_ARGS;
       ctx->urgent_cus = value;
     } else {
@@ -2434,6 +2453,9 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
     ctx->opt.urgent_max_sets = value;
   } else if (k == "urgent_excl") {
     ctx->opt.urgent_excl = value != 0;
+  } else if (k == "urgent_wait_us") {
+    if (value < 0 || value > 100000) return BLSGPU_ERR_ARGS;
+    ctx->opt.urgent_wait_us = value;
   } else if (k == "fb_check6") {
     if (value < 0 || value > 2) return BLSGPU_ERR_ARGS;
     ctx->opt.fb_check6 = value;
@@ -2483,6 +2505,11 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   }
   if (k == "hw_queues") {
     *value = ctx->hw_queues;
+    return BLSGPU_OK;
+  }
+  if (k == "blocking_sync") {
+    std::lock_guard<std::mutex> sk(ctx->slots_mu);
+    *value = ctx->blocking_sync;
     return BLSGPU_OK;
   }
   if (k == "urgent_cus" || k == "urgent_isolate") {
@@ -2538,6 +2565,7 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "urgent_lane") *value = o.urgent_lane;
   else if (k == "urgent_max_sets") *value = o.urgent_max_sets;
   else if (k == "urgent_excl") *value = o.urgent_excl;
+  else if (k == "urgent_wait_us") *value = o.urgent_wait_us;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }
