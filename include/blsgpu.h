@@ -205,7 +205,8 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * partition, the pipeline streams are masked off it; 2: and the urgent streams are left unmasked at the highest
  * priority, so an idle chip is theirs too; 3, diagnostics: the pipeline streams masked with every CU; 0..3) -- these two only before the first call (the
  * streams are created with it; BLSGPU_ERR_ARGS afterwards), "blocking_sync" (the dispatcher threads block on their
- * runs' completion events instead of spinning, 0/1, default 1; before the first call only),
+ * runs' completion events instead of spinning, 0/1, default 1; before the first call only), "pipeline_prio" (the
+ * pipeline's message and tail streams take the device's highest priority, 0/1, default 1; before the first call only),
  * "lane_tail_min" / "lane_tail_parts" (runs of >= lane_tail_min sets take lane forms of the Horner passes (bit 0)
  * and of MillerLoop(-g1, S) (bit 1) instead of the cooperative workgroups; default 0 = never, parts 3), "serial"
  * (diagnostics: every branch of a run on one stream, so each kernel runs alone on the chip; 0/1, default 0), "profile" (per-stage kernel times in

@@ -394,6 +394,7 @@ struct blsgpu_ctx {
   int64_t urgent_cus = 0;
   int64_t urgent_isolate = 1;  // (no effect without a partition)
   int64_t blocking_sync = 1;   // dispatchers block on their runs' completion events instead of spinning
+  int64_t pipeline_prio = 1;   // the pipeline's message and tail streams take the device's highest priority
 };
 
 namespace {
@@ -1973,7 +1974,7 @@ void create_streams(blsgpu_ctx* ctx, Device* d) {
   // default three slots' runs then has its own pair, and a run never queues behind another run's tail.
   d->npairs = ctx->hw_queues >= 6 ? kMaxPairs : 2;
   for (int k = 0; k < 2 * d->npairs; k++) {
-    const bool high = (BLSGPU_STREAM_PRIO & (1 << (k & 3))) != 0 || (k >= kStreams && (k & 1));
+    const bool high = ctx->pipeline_prio && ((BLSGPU_STREAM_PRIO & (1 << (k & 3))) != 0 || (k >= kStreams && (k & 1)));
     d->st[k] = make_stream(d->main_mask, high ? prio_hi : prio_lo);
   }
   for (int k = 0; k < 4; k++) d->ust[k] = make_stream(pmask, prio_hi);
@@ -2349,12 +2350,13 @@ int blsgpu_pubkeys_upload(blsgpu_ctx* ctx, uint32_t first_index, const uint8_t* 
 int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
   if (!ctx || !key) return BLSGPU_ERR_ARGS;
   std::string k(key);
-  if (k == "urgent_cus" || k == "urgent_isolate" || k == "blocking_sync") {  // stream / event creation: first call
+  if (k == "urgent_cus" || k == "urgent_isolate" || k == "blocking_sync" || k == "pipeline_prio") {
+    // stream / event creation: before the first call only
     std::lock_guard<std::mutex> sk(ctx->slots_mu);
     if (ctx->slots_started) return BLSGPU_ERR_ARGS;
-    if (k == "blocking_sync") {
+    if (k == "blocking_sync" || k == "pipeline_prio") {
       if (value < 0 || value > 1) return BLSGPU_ERR_ARGS;
-      ctx->blocking_sync = value;
+      (k == "blocking_sync" ? ctx->blocking_sync : ctx->pipeline_prio) = value;
     } else if (k == "urgent_cus") {
       if (value < 0 || value > 128 || (value & 7)) return BLSGPU_ERR_ARGS;
       ctx->urgent_cus = value;
@@ -2507,9 +2509,9 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
     *value = ctx->hw_queues;
     return BLSGPU_OK;
   }
-  if (k == "blocking_sync") {
+  if (k == "blocking_sync" || k == "pipeline_prio") {
     std::lock_guard<std::mutex> sk(ctx->slots_mu);
-    *value = ctx->blocking_sync;
+    *value = k == "blocking_sync" ? ctx->blocking_sync : ctx->pipeline_prio;
     return BLSGPU_OK;
   }
   if (k == "urgent_cus" || k == "urgent_isolate") {

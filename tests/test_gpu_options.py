@@ -19,7 +19,7 @@ KEYS = {
     "profile": (1, None), "max_devices": (1, 0),
     "urgent_lane": (0, None), "urgent_max_sets": (64, -1), "urgent_excl": (1, None), "urgent_wait_us": (0, -1),
     # stream creation options: the fixture's context has made no call yet, so they still take values
-    "urgent_cus": (16, 12), "urgent_isolate": (2, 4), "blocking_sync": (0, 2),
+    "urgent_cus": (16, 12), "urgent_isolate": (2, 4), "blocking_sync": (0, 2), "pipeline_prio": (0, 2),
 }
 
 
