@@ -360,6 +360,23 @@ def pmc_source():
 BLST_SETS_PER_CORE = 2200.0  # published anchor: ~0.9 ms/set/thread, x2 batched
 
 
+def thread_cpu():
+    """{tid: (thread name, CPU seconds)} of this process's threads (/proc/self/task; the runtime names its dispatcher
+    threads blsgpu-slot / blsgpu-urgent and its packing threads blsgpu-pack)."""
+    out, tick = {}, os.sysconf("SC_CLK_TCK")
+    try:
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                nm = open(f"/proc/self/task/{tid}/comm").read().strip()
+                f = open(f"/proc/self/task/{tid}/stat").read().rsplit(")", 1)[1].split()
+                out[tid] = (nm, (int(f[11]) + int(f[12])) / tick)
+            except (OSError, ValueError, IndexError):
+                pass
+    except OSError:
+        pass
+    return out
+
+
 def host_cpus():
     """The host CPUs this process may use, checked rather than assumed: the affinity mask
     (os.sched_getaffinity), its physical cores (/proc/cpuinfo physical id + core id), and the CPU share the
@@ -726,6 +743,7 @@ def main():
     sync()
     t0 = time.perf_counter()
     cpu0 = time.process_time()  # host CPU seconds of every thread of the process (dispatchers, packing, callers)
+    thr0 = thread_cpu()
     w0 = time.monotonic_ns()  # the timed window on CLOCK_MONOTONIC, the clock of rocprofv3's kernel timestamps
     if urgent is not None:
         uthread = threading.Thread(target=urgent_probe, args=(ctx, ucalls, ustop, args.urgent_every_ms, ulat))
@@ -739,6 +757,10 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     cpu_s = time.process_time() - cpu0
+    thr1 = thread_cpu()
+    by_thread = {}
+    for tid, (nm, c1) in thr1.items():
+        by_thread[nm] = by_thread.get(nm, 0.0) + c1 - thr0.get(tid, (nm, 0.0))[1]
     w1 = time.monotonic_ns()
     ctx.set_option("profile", 0)
     stats = [r[0] for r in results]
@@ -786,6 +808,7 @@ def main():
                  "run_host_ms": {"p50": round(float(np.percentile([st.host_ms for st in runs_timed], 50)), 3),
                                  "p99": round(float(np.percentile([st.host_ms for st in runs_timed], 99)), 3),
                                  "runs": len(runs_timed)} if runs_timed else None,
+                 "cpu_s_by_thread": {k: round(v, 3) for k, v in sorted(by_thread.items(), key=lambda kv: -kv[1])[:8]},
                  "devices": devices},
         "call_latency_under_load_ms": {"p50": round(float(np.percentile(call_lat, 50)), 2),
                                        "p99": round(float(np.percentile(call_lat, 99)), 2)},

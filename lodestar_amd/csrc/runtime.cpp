@@ -23,6 +23,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 #include <sys/random.h>
 
 #include <algorithm>
@@ -1611,6 +1612,7 @@ void run_merged(Device& d, Slot& sl, const std::vector<Task>& parts, std::vector
     jfs[0] = 0;
     spf[0] = 0;
     auto pack = [&](size_t q) {
+      if (q) pthread_setname_np(pthread_self(), "blsgpu-pack");
       const Task& t = parts[live[q]];
       const Shard& sh = t.call->shards[t.shard];
       const blsgpu_batch& b = t.call->b;
@@ -1747,6 +1749,7 @@ inline uint32_t task_sets(const Task& t) {
 // the slot is retired (option "slots" lowered).
 void worker_loop(Device* d, Slot* sl) {
   tl_dispatcher = true;
+  pthread_setname_np(pthread_self(), "blsgpu-slot");  // host-cost accounting by thread (bench.py "host")
   (void)hipSetDevice(d->id);
   for (;;) {
     std::vector<Task> parts;
@@ -1851,6 +1854,7 @@ void worker_loop(Device* d, Slot* sl) {
 // checks.  Exits when the device stops and its urgent queue is drained.
 void urgent_loop(Device* d, Slot* sl) {
   tl_dispatcher = true;
+  pthread_setname_np(pthread_self(), "blsgpu-urgent");
   (void)hipSetDevice(d->id);
   for (;;) {
     std::vector<Task> parts;

@@ -276,6 +276,20 @@ def make_batch(job_first_set, sigs, sig_len, msgs, pk_bytes=None, set_pk_first=N
     return b, keep
 
 
+class Pending:
+    """An asynchronous call of Context.submit_raw."""
+
+    status = None
+    t_done = None
+
+    def wait(self, timeout=None):
+        if not self.ev.wait(timeout):
+            raise TimeoutError("blsgpu_submit: call not completed")
+        if self.status != OK:
+            raise RuntimeError(f"blsgpu_submit -> {code_name(self.status)}")
+        return self.res[: self.n_jobs], self.st
+
+
 class Context:
     """Owns a blsgpu_ctx on one or more HIP devices."""
 
@@ -340,6 +354,31 @@ class Context:
         if rc != OK:
             raise RuntimeError(f"blsgpu_verify -> {code_name(rc)}")
         return res[: b.n_jobs], st
+
+    def submit_raw(self, job_first_set, sigs, sig_len, msgs, pk_bytes=None, set_pk_first=None, pk_index=None,
+                   job_flags=None, sig_stride=None, seed=0x4C4F444553544152):
+        """Asynchronous call (blsgpu_submit: inputs copied before it returns): a Pending whose wait() gives
+        (job_result int8 array, Stats) once the runtime's done callback ran."""
+        import threading
+
+        b, keep = make_batch(job_first_set, sigs, sig_len, msgs, pk_bytes, set_pk_first, pk_index, job_flags,
+                             sig_stride, seed)
+        p = Pending()
+        p.res = np.zeros(max(b.n_jobs, 1), dtype=np.int8)
+        p.n_jobs = b.n_jobs
+        p.st = Stats()
+        p.ev = threading.Event()
+
+        def done(user, status):
+            p.status = status
+            p.t_done = __import__("time").perf_counter()
+            p.ev.set()
+
+        p.cb = DONE_CB(done)  # kept alive with the Pending until the callback ran
+        rc = self._lib.blsgpu_submit(self.h, ctypes.byref(b), p.res.ctypes.data, ctypes.byref(p.st), p.cb, None)
+        if rc != OK:
+            raise RuntimeError(f"blsgpu_submit -> {code_name(rc)}")
+        return p
 
     def aggregate_pubkeys(self, pk_bytes=None, set_pk_first=None, pk_index=None, out_len=96):
         """PublicKey.aggregate(...).toBytes() per set on the GPU: (list of bytes, status int8 array)."""

@@ -3,7 +3,6 @@
 the main thread, outside the pool queue (multithread/index.ts:138-151) -- submitted behind a gossip flood of 16,384-set
 calls completes before the flood does, with the oracle's answer: valid, a signature over the wrong message, a malformed
 signature, and 3-set calls.  Results are compared job for job with oracle/blscpu.c on the same inputs and seed."""
-import threading
 import time
 
 import numpy as np
@@ -16,7 +15,7 @@ from oracle import cpu
 pytestmark = pytest.mark.gpu
 
 THREADS = bench.host_cpus()["threads"]
-N_FLOOD, FLOOD_CALLS, N_KEYS = 16384, 16, 16384
+N_FLOOD, FLOOD_CALLS, N_KEYS = 16384, 24, 16384
 
 
 @pytest.fixture(scope="module")
@@ -85,70 +84,37 @@ def test_urgent_calls_alone_vs_oracle(env):
         assert st.urgent_lane == 1
 
 
-def run_behind_flood(ctx, flood, calls, seeds, twin=None):
-    """Queues the flood (FLOOD_CALLS threads), then after 30 ms submits the urgent calls together (and, with `twin`, the
-    same calls without the urgent flag, as ordinary calls queued behind the flood).  Returns (urgent outcomes [(result,
-    lane, ms, done_t)], twin outcomes, sorted flood completion times (ms from the flood's submission))."""
-    done, errs = [None] * FLOOD_CALLS, []
-
-    def flood_call(k):
-        try:
-            res, _ = ctx.verify_raw(**flood[k], seed=bench.SEED)
-            if not (res == 1).all():
-                errs.append(f"flood call {k}: {(res != 1).sum()} jobs not valid")
-        except Exception as e:  # noqa: BLE001 -- reported below
-            errs.append(repr(e))
-        done[k] = time.perf_counter()
-
-    def one(c, seed, out, t):
-        t1 = time.perf_counter()
-        got, st = ctx.verify_raw(**c, seed=seed)
-        out[t] = (int(got[0]), int(st.urgent_lane), (time.perf_counter() - t1) * 1e3, time.perf_counter())
-
-    th = [threading.Thread(target=flood_call, args=(k,)) for k in range(FLOOD_CALLS)]
-    t0 = time.perf_counter()
-    for x in th:
-        x.start()
-    time.sleep(0.03)  # the flood is queued on the device
-    outs, touts = [None] * len(calls), [None] * len(calls)
-    uth = [threading.Thread(target=one, args=(c, seeds[t], outs, t)) for t, c in enumerate(calls)]
-    if twin:
-        uth += [threading.Thread(target=one, args=(dict(c, job_flags=np.zeros(1, np.uint8)), seeds[t], touts, t))
-                for t, c in enumerate(calls)]
-    for x in uth:
-        x.start()
-    for x in uth + th:
-        x.join(timeout=120)
-    assert not errs, errs
-    rel = lambda o: [(r, lane, ms, (d - t0) * 1e3) for r, lane, ms, d in o] if o[0] else None
-    return rel(outs), rel(touts) if twin else None, sorted((d - t0) * 1e3 for d in done)
-
-
 def test_urgent_calls_overtake_a_gossip_flood(env):
-    """FLOOD_CALLS x 16,384-set calls (two merged pipeline runs of 131,072 sets) are queued first, then the urgent calls
-    (valid, wrong message, malformed signature, 3-set jobs) and the same calls without the urgent flag, submitted
-    together: every urgent call gives the oracle's answer on the urgent lane (the burst merged into one lane run), and
-    all of them finish before the ordinary copies, which wait behind the flood in the device queue.  (With an isolated CU
-    partition, `urgent_cus` 8, they also finish before the flood's median call: measured by bench.py in processes of
-    their own, profiles/r06_urgent_latency.json -- a second context with CU-masked pipeline streams beside this one
-    exhausted the scratch the extra hardware queues reserve)"""
+    """FLOOD_CALLS x 16,384-set gossip calls are queued first (blsgpu_submit, asynchronous), then -- 30 ms later, within
+    microseconds of each other -- the urgent calls (valid, wrong message, malformed signature, 3-set jobs) and the same
+    calls without the urgent flag: every urgent call gives the oracle's answer on the urgent lane, the burst as one lane
+    run, and all of them finish before their ordinary copies, which wait for the gossip calls queued ahead of them."""
     ctx, sks, pks, flood = env
     calls = [urgent_call(sks, idx, kinds, 100 + t) for t, (idx, kinds, _) in enumerate(URGENT_CASES)]
     seeds = [bench.SEED + 100 + t for t in range(len(calls))]
     wants = [oracle_result(pks, c, s) for c, s in zip(calls, seeds)]
     ctx.verify_raw(**calls[0], seed=seeds[0])  # the lane's buffers exist before timing
-    outs, touts, flood_ms = run_behind_flood(ctx, flood, calls, seeds, twin=True)
-    u_done = max(o[3] for o in outs)
-    t_done = min(o[3] for o in touts)
-    print(f"urgent latencies behind the flood (ms): {[round(o[2], 2) for o in outs]}, done at {u_done:.1f} ms; flood "
-          f"done at {flood_ms[0]:.1f} .. {flood_ms[-1]:.1f} ms; the same calls queued as ordinary calls done at "
-          f"{t_done:.1f} .. {max(o[3] for o in touts):.1f} ms")
-    for t, o in enumerate(outs):
-        assert o[0] == wants[t], (t, o, wants[t])
-        assert o[1] == 1
-    for t, o in enumerate(touts):
-        assert o[0] == wants[t] and o[1] == 0
-    assert u_done < t_done, "urgent calls did not overtake the queue"
+    t0 = time.perf_counter()
+    fl = [ctx.submit_raw(**flood[k], seed=bench.SEED) for k in range(FLOOD_CALLS)]
+    time.sleep(0.03)
+    t1 = time.perf_counter()
+    urg = [ctx.submit_raw(**c, seed=s) for c, s in zip(calls, seeds)]
+    twin = [ctx.submit_raw(**dict(c, job_flags=np.zeros(1, np.uint8)), seed=s) for c, s in zip(calls, seeds)]
+    u = [p.wait(120) for p in urg]
+    w = [p.wait(120) for p in twin]
+    for p in fl:
+        res, _ = p.wait(120)
+        assert (res == 1).all()
+    ms = lambda p: (p.t_done - t0) * 1e3
+    u_done, t_first = max(ms(p) for p in urg), min(ms(p) for p in twin)
+    print(f"urgent calls done {[round(ms(p) - (t1 - t0) * 1e3, 1) for p in urg]} ms after submission (at {u_done:.1f} "
+          f"ms); their ordinary copies done at {t_first:.1f} .. {max(ms(p) for p in twin):.1f} ms; the flood at "
+          f"{min(ms(p) for p in fl):.1f} .. {max(ms(p) for p in fl):.1f} ms")
+    for t, ((res, st), (res2, st2)) in enumerate(zip(u, w)):
+        assert int(res[0]) == wants[t] and st.urgent_lane == 1, (t, res, wants[t])
+        assert int(res2[0]) == wants[t] and st2.urgent_lane == 0
+    assert u[0][1].run_calls == len(calls), "the urgent burst ran as one lane run"
+    assert u_done < t_first, "urgent calls did not overtake the queue"
 
 
 def test_large_urgent_call_takes_the_queue_head(env):
