@@ -163,7 +163,10 @@ typedef void (*blsgpu_done_cb)(void* user, int status);
 int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result, blsgpu_stats* stats,
                   blsgpu_done_cb done, void* user);
 
-/* Tunables ("slots" may not be changed from a done callback: BLSGPU_ERR_ARGS): "group_sets" (sets per batch group before a new one opens, default 1024), "slots" (runtime slots
+/* Tunables ("slots" may not be changed from a done callback: BLSGPU_ERR_ARGS): "group_sets" (sets per batch group before a new one opens, default 1024), "group_adapt"
+ * (while a device sees invalid sets, its batch groups shrink to the size that minimises the expected work of a group's
+ * final exponentiation against re-checking a failed group's clean jobs -- ~16 sets at 1% invalid, group_sets when all
+ * are valid; per-job results are unaffected; 0/1, default 1), "slots" (runtime slots
  * per device, 1..64; default by hardware queues), "max_devices" (devices one call may shard over, default all),
  * "dedupe" (message dedupe + same-message pairing, 0/1, default 1), "miller_k" (pairings per Miller
  * accumulator sharing its Fp12 squarings, 1..64; default 0 = by run size: 1 below 131072 pairings, 2 below

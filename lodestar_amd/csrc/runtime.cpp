@@ -27,6 +27,7 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -205,6 +206,8 @@ struct Device {
   int urgent_cus = 0;            // CUs of the partition the streams were created with (0 = none)
   std::vector<uint32_t> main_mask;  // CU mask of the pipeline and fallback streams (empty = all CUs, priorities)
   bool blocking_sync = true;        // the dispatchers' wait events block instead of spinning (create_slot_events)
+  std::mutex fail_mu;
+  double fail_rate = 0;  // EWMA over this device's runs of the fraction of invalid sets (group_adapt)
 };
 
 // Device-failure injection (blsgpu_debug_inject, tests only): the next `count` pipeline runs after `skip` more fail as
@@ -255,6 +258,7 @@ struct Options {  // snapshot taken at the start of each call
   int64_t urgent_max_sets = 512;  // larger urgent calls go to the head of the device queue instead
   int64_t urgent_excl = 0;        // urgent runs may use the exclusive-CU padding of the cooperative kernels
   int64_t urgent_wait_us = 300;   // the urgent dispatcher lingers this long for more urgent calls of a burst
+  int64_t group_adapt = 1;        // batch groups shrink below group_sets while the device sees invalid sets
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
            group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&
@@ -264,7 +268,8 @@ struct Options {  // snapshot taken at the start of each call
            lines_lanes == o.lines_lanes && merge_balance == o.merge_balance && early_release == o.early_release && tail_on_msg == o.tail_on_msg && copy_stream == o.copy_stream && coop_max == o.coop_max &&
            coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec && spec_large == o.spec_large &&
            fb_lane_min == o.fb_lane_min && acc6_max == o.acc6_max && miller_pairs == o.miller_pairs && small_max == o.small_max &&
-           fb_direct_min == o.fb_direct_min && fb_check6 == o.fb_check6 && fb_force_busy == o.fb_force_busy;
+           fb_direct_min == o.fb_direct_min && fb_check6 == o.fb_check6 && fb_force_busy == o.fb_force_busy &&
+           group_adapt == o.group_adapt;
   }
 };
 
@@ -488,6 +493,32 @@ struct MsgIndex {
   }
 };
 
+// Batch-group size for a run (group_adapt).  A group costs a fixed ~14.7k Montgomery multiplications (its
+// MillerLoop(-g1, S) 5,747, final exponentiation 7,835, MSM range 1,085; lodestar_amd/op_counts.json), and when it fails
+// every clean job in it is re-checked: per set ~13.6k / (sets per job) + 1.3k (the job's own S_j, MillerLoop(-g1, S_j)
+// and final exponentiation; the per-set Miller values are reused).  With invalid sets at rate f a group of g sets fails
+// with probability 1 - (1 - f)^g, so the expected cost per set is 14.7k / g + (1 - (1 - f)^g) * retry: the size that
+// minimises it over powers of two in [8, group_sets].  All valid (f = 0): group_sets (1,024); the reference pool's 1%
+// invalid gossip (C5, jobs of 1-3 sets): ~16.  Per-job results do not depend on the grouping (each job's verdict is its
+// own, as the reference's per-job re-verification); only the work does.
+uint32_t adapt_group_sets(Device& d, int64_t group_sets, double sets_per_job) {
+  double f;
+  {
+    std::lock_guard<std::mutex> lk(d.fail_mu);
+    f = d.fail_rate;
+  }
+  const uint32_t gmax = (uint32_t)std::max<int64_t>(1, group_sets);
+  if (f <= 0 || gmax <= 8) return gmax;
+  const double retry = 13600.0 / std::max(1.0, sets_per_job) + 1300.0, fixed = 14700.0;
+  uint32_t best = gmax;
+  double best_c = fixed / gmax + (1.0 - std::pow(1.0 - f, (double)gmax)) * retry;
+  for (uint32_t g = 8; g < gmax; g *= 2) {
+    const double c = fixed / g + (1.0 - std::pow(1.0 - f, (double)g)) * retry;
+    if (c < best_c) best_c = c, best = g;
+  }
+  return best;
+}
+
 // Runs one device's shard on one slot.  Writes job_result[job_begin..job_end).
 // A slot's run leaves the device's in-flight count (once): its batch pass is complete on the GPU, so another slot
 // may start the next run while this one finishes on the host (results, fallback round trips).
@@ -554,6 +585,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       group_batchable.push_back(g.batchable);
     }
   } else {
+    // group size: group_sets, or smaller while this device has seen invalid sets (group_adapt, adapt_group_sets)
+    const uint32_t gs = opt.group_adapt ? adapt_group_sets(d, opt.group_sets, (double)n / std::max(nj, 1u))
+                                        : (uint32_t)opt.group_sets;
     uint32_t cur_sets = 0;
     bool open = false;
     for (uint32_t j = 0; j < nj; j++) {
@@ -569,7 +603,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
         open = false;
         continue;
       }
-      if (!open || cur_sets >= (uint32_t)opt.group_sets) {
+      if (!open || cur_sets >= gs) {
         group_jobs.push_back({j, j});
         cur_sets = 0;
         open = true;
@@ -1317,6 +1351,21 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     }
   }
   for (uint32_t j = 0; j < nj; j++) job_result[sh.job_begin + j] = (int8_t)jr[j];
+  // the device's invalid-set rate estimate (group_adapt): a group "failed" when any of its non-empty jobs was not
+  // valid; with groups of s sets failing at rate pf, a set is invalid at rate f = 1 - (1 - pf)^(1/s)
+  if (!plan && ng0) {
+    uint32_t failed = 0;
+    for (uint32_t g = 0; g < ng0; g++)
+      for (uint32_t j = group_jobs[g].first; j < group_jobs[g].second; j++)
+        if (jr[j] != 1 && job_sets(j).second > job_sets(j).first) {
+          failed++;
+          break;
+        }
+    const double pf = std::min((double)failed, ng0 - 0.5) / ng0;
+    const double f = 1.0 - std::pow(1.0 - pf, (double)ng0 / std::max(n, 1u));
+    std::lock_guard<std::mutex> lk(d.fail_mu);
+    d.fail_rate = 0.5 * d.fail_rate + 0.5 * f;
+  }
   return BLSGPU_OK;
 }
 
@@ -2459,6 +2508,8 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
     ctx->opt.urgent_max_sets = value;
   } else if (k == "urgent_excl") {
     ctx->opt.urgent_excl = value != 0;
+  } else if (k == "group_adapt") {
+    ctx->opt.group_adapt = value != 0;
   } else if (k == "urgent_wait_us") {
     if (value < 0 || value > 100000) return BLSGPU_ERR_ARGS;
     ctx->opt.urgent_wait_us = value;
@@ -2572,6 +2623,7 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "urgent_max_sets") *value = o.urgent_max_sets;
   else if (k == "urgent_excl") *value = o.urgent_excl;
   else if (k == "urgent_wait_us") *value = o.urgent_wait_us;
+  else if (k == "group_adapt") *value = o.group_adapt;
   else return BLSGPU_ERR_ARGS;
   return BLSGPU_OK;
 }

@@ -20,6 +20,8 @@ def ctx():
     from lodestar_amd.native import Context
 
     c = Context()
+    # these tests count groups and retries of a fixed grouping (multithread.test.ts:89-106 shapes): no adaptive sizing
+    c.set_option("group_adapt", 0)
     yield c
     c.close()
 
