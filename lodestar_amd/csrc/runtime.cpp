@@ -1915,19 +1915,30 @@ void urgent_loop(Device* d, Slot* sl) {
       d->uqueue.pop_front();
       const Call* c0 = parts[0].call;
       uint32_t total = task_sets(parts[0]);
-      // a burst of urgent calls (several main-thread verifications issued in one JS tick) arrives within microseconds:
-      // linger up to urgent_wait_us so it becomes one run instead of a run and a queue behind it
-      if (c0->opt.urgent_wait_us > 0 && d->uqueue.empty() && !d->stop)
-        d->q_cv.wait_for(lk, std::chrono::microseconds(c0->opt.urgent_wait_us),
-                         [&] { return d->stop || !d->uqueue.empty(); });
-      while (!d->uqueue.empty()) {
-        const Task& nx = d->uqueue.front();
-        if ((int64_t)(total + task_sets(nx)) > c0->opt.urgent_max_sets || pk_mode(nx.call->b) != pk_mode(c0->b) ||
-            !nx.call->opt.same_run(c0->opt))
-          break;
-        total += task_sets(nx);
-        parts.push_back(nx);
-        d->uqueue.pop_front();
+      // a burst of urgent calls (several main-thread verifications issued in one JS tick) arrives a few microseconds
+      // apart: the burst lasts while each next call comes within urgent_wait_us of the previous one (at most 8 gaps'
+      // worth in all), so it becomes one run instead of a run and a queue behind it
+      const auto gap = std::chrono::microseconds(std::max<int64_t>(c0->opt.urgent_wait_us, 0));
+      const auto linger_end = std::chrono::steady_clock::now() + 8 * gap;
+      for (;;) {
+        bool blocked = false;
+        while (!d->uqueue.empty()) {
+          const Task& nx = d->uqueue.front();
+          if ((int64_t)(total + task_sets(nx)) > c0->opt.urgent_max_sets || pk_mode(nx.call->b) != pk_mode(c0->b) ||
+              !nx.call->opt.same_run(c0->opt)) {
+            blocked = true;
+            break;
+          }
+          total += task_sets(nx);
+          parts.push_back(nx);
+          d->uqueue.pop_front();
+        }
+        if (blocked || gap.count() == 0 || d->stop || (int64_t)total >= c0->opt.urgent_max_sets) break;
+        const auto now = std::chrono::steady_clock::now();
+        if (now >= linger_end) break;
+        if (!d->q_cv.wait_for(lk, std::min<std::chrono::steady_clock::duration>(gap, linger_end - now),
+                              [&] { return d->stop || !d->uqueue.empty(); }))
+          break;  // the gap passed with no new urgent call: the burst is over
       }
     }
     sl->alone = true;
