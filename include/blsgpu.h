@@ -187,7 +187,9 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * default 512 / 4096), "coop_excl_max" (cooperative workgroups take a CU each in runs of <= this many items, default
  * 512), "rsig_spec" (small idle runs form every r_i sig_i beside the batch pass for a possible fallback, 0/1, default
  * 1), "spec_large" (runs above small_max that find the device idle start their MSM speculatively after the decode, as
- * small ones do, 0/1, default 1), "fb_lane_min" (fallback check launches of >= this many checks in large runs take one lane per check, default
+ * small ones do, 0/1, default 1), "spec_gsm" (such a speculative run's MillerLoop(-g1, S) follows its MSM on the other
+ * stream pair's message stream instead of the run's signature stream, 0/1, default 0: measured equal), "fb_lane_min"
+ * (fallback check launches of >= this many checks in large runs take one lane per check, default
  * 256, 0 = never), "route_split_sets" (see blsgpu_route_call, default 16384), "acc6_max" (runs of one-item Miller chunks up to this many
  * take the six-lane accumulation, default 16384; "miller_lanes" 6 forces it), "miller_pairs" (larger runs take the
  * lane-pair accumulation, every Fp2 split over two lanes at two waves per SIMD, 0/1, default 0; "miller_lanes" 3

@@ -245,6 +245,7 @@ struct Options {  // snapshot taken at the start of each call
   int64_t coop_excl_max = 512;    // cooperative workgroups take a CU each only in runs of <= this many items
   int64_t rsig_spec = 1;          // small idle runs form every r_i sig_i beside the batch pass (for the fallback)
   int64_t spec_large = 1;         // runs above small_max on an idle device take the speculative MSM too
+  int64_t spec_gsm = 0;           // a speculative run's MillerLoop(-g1, S) follows its MSM on the other pair's stream
   int64_t fb_lane_min = 256;      // fallback check launches of >= this many checks take one lane per check (0 = never)
   int64_t route_split_sets = 16384;  // a call is split over min(devices, sets / this) devices, else routed whole
   int64_t acc6_max = 16384;       // one-item-chunk runs of <= this many chunks take the six-lane accumulation
@@ -266,7 +267,7 @@ struct Options {  // snapshot taken at the start of each call
            lane_tail_parts == o.lane_tail_parts &&
            msm_slice_mid == o.msm_slice_mid && msm_tree == o.msm_tree &&
            lines_lanes == o.lines_lanes && merge_balance == o.merge_balance && early_release == o.early_release && tail_on_msg == o.tail_on_msg && copy_stream == o.copy_stream && coop_max == o.coop_max &&
-           coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec && spec_large == o.spec_large &&
+           coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec && spec_large == o.spec_large && spec_gsm == o.spec_gsm &&
            fb_lane_min == o.fb_lane_min && acc6_max == o.acc6_max && miller_pairs == o.miller_pairs && small_max == o.small_max &&
            fb_direct_min == o.fb_direct_min && fb_check6 == o.fb_check6 && fb_force_busy == o.fb_force_busy &&
            group_adapt == o.group_adapt;
@@ -1079,6 +1080,13 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     // this pair copies its inputs on
     const bool tail_msg = opt.tail_on_msg && !opt.serial && BLSGPU_STREAM_PAIRS;
     hipStream_t sg = s;
+    // spec_gsm: a speculative run (the device was idle when it formed) runs MillerLoop(-g1, S) right behind its MSM on
+    // the other pair's message stream (high priority, nothing else queued on it yet): it starts on a nearly idle chip.
+    // On the signature stream it would wait behind the run's own Miller accumulation and then behind the next run's
+    // stage kernels -- a three-wave workgroup gets no CU while another run's waves fill every SIMD -- and it held the
+    // burst's first run, and so the pair, for ~36 ms of the driver's 20-step window.  Measured equal (the next runs then
+    // wait behind it on the other pair instead, profiles/r06_ramp_ab.json): off by default.
+    if (spec && opt.spec_gsm && !tail_msg) sg = smsm;
     if (tail_msg) {
       HIPCHK(hipEventRecord(sl.join_gsm, s));
       HIPCHK(hipStreamWaitEvent(sm, sl.join_gsm, 0));
@@ -2507,6 +2515,8 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
     ctx->opt.rsig_spec = value != 0;
   } else if (k == "spec_large") {
     ctx->opt.spec_large = value != 0;
+  } else if (k == "spec_gsm") {
+    ctx->opt.spec_gsm = value != 0;
   } else if (k == "fb_lane_min") {
     if (value < 0) return BLSGPU_ERR_ARGS;
     ctx->opt.fb_lane_min = value;
@@ -2622,6 +2632,7 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "coop_excl_max") *value = o.coop_excl_max;
   else if (k == "rsig_spec") *value = o.rsig_spec;
   else if (k == "spec_large") *value = o.spec_large;
+  else if (k == "spec_gsm") *value = o.spec_gsm;
   else if (k == "fb_lane_min") *value = o.fb_lane_min;
   else if (k == "route_split_sets") *value = o.route_split_sets;
   else if (k == "acc6_max") *value = o.acc6_max;

@@ -13,7 +13,7 @@ KEYS = {
     "msm_slice_mid": (64, 3), "msm_tree": (0, None), "f_run_max": (8, 3), "pipeline_depth": (2, 0),
     "merge_wait_us": (1000, -1), "idle_wait_us": (100, -1), "lane_tail_min": (1, -1), "lane_tail_parts": (1, 4),
     "merge_balance": (1, None), "early_release": (1, None), "tail_on_msg": (1, None), "copy_stream": (1, None),
-    "coop_max": (256, -1), "coop_g2_max": (1024, -1), "coop_excl_max": (128, -1), "rsig_spec": (0, None), "spec_large": (0, None),
+    "coop_max": (256, -1), "coop_g2_max": (1024, -1), "coop_excl_max": (128, -1), "rsig_spec": (0, None), "spec_large": (0, None), "spec_gsm": (1, None),
     "fb_lane_min": (64, -1), "fb_direct_min": (512, -1), "fb_check6": (1, 3), "fb_force_busy": (1, None),
     "route_split_sets": (8192, 0), "acc6_max": (4096, -1), "small_max": (2048, -1), "serial": (1, None),
     "profile": (1, None), "max_devices": (1, 0),
