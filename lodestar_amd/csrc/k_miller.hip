@@ -33,6 +33,55 @@
 
 BLS_INL fp fp_add_n(const fp& a, const fp& b) { return fp_add_norm(a, b); }
 
+// LDS-staged line prefetch for the accumulation kernels (north star: "LDS staging of precomputed line coefficients").
+// The accumulation runs one wave per SIMD, so nothing hides the HBM latency of the 84 line words an item needs at each
+// step (SQ: 19-22% of its wave-cycles waiting).  Each lane's next line (the next item of the step, or the chunk's first
+// item of the next step) is fetched straight into LDS by global_load_lds_dword -- no VGPRs held while it is in flight
+// -- as soon as the current one has been read out, so it arrives during the current item's sparse product (or the
+// next step's squaring).  Word-major slot: word w of lane t at pre[w * WAVE + t] (the DMA writes lane t's dword at
+// M0 + 4 t); one slot per one-wave workgroup, 21.5 KB.  Measured (round 6, profiles/r06_lds_prefetch_ab.json): parity
+// green, no gain (C2 3.27M vs 3.30M at 20 steps, 3.81M vs 3.82M at 100; the Miller stage no faster) -- the waiting is
+// not the line loads -- so off by default.
+#ifndef BLS_ACC_PREFETCH
+#define BLS_ACC_PREFETCH 0
+#endif
+#if BLS_ACC_PREFETCH && defined(__HIP_DEVICE_COMPILE__)
+#define LDS_AS __attribute__((address_space(3)))
+// a rolled loop over the 84 words: one running address (the unrolled form kept 84 64-bit addresses live and spilled)
+__device__ __forceinline__ void line_prefetch(uint32_t* pre, const uint32_t* o, uint32_t nm, uint32_t m) {
+  const uint32_t* a = o + opaque_u32(m);
+#pragma unroll 1
+  for (int w = 0; w < W_LINE; w++) {
+    __builtin_amdgcn_global_load_lds((const void*)a, (LDS_AS void*)(pre + w * WAVE), 4, 0, 0);
+    a += nm;
+  }
+}
+// the prefetched line is in LDS (vmcnt(0): global_load_lds completes through the vector memory counter)
+__device__ __forceinline__ void line_wait() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  asm volatile("" ::: "memory");
+}
+// the slot's words are in registers (lgkmcnt(0)) before the next prefetch may overwrite it
+__device__ __forceinline__ void line_read_done() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ fp ld_fp_pre(const uint32_t* pre, int w0) {
+  fp r;
+#pragma unroll
+  for (int l = 0; l < BLS_NL; l++) r.l[l] = pre[(w0 + l) * WAVE + threadIdx.x];
+  return r;
+}
+__device__ __forceinline__ fp2 ld_fp2_pre(const uint32_t* pre, int w0) {
+  return fp2_make(ld_fp_pre(pre, w0), ld_fp_pre(pre, w0 + W_FP));
+}
+#define ACC_PREFETCH 1
+#else
+#define ACC_PREFETCH 0
+#endif
+
 STAGE_KERNEL_W(BLSGPU_WPE_LINES) void k_miller_lines(PipelineBuffers b) {
   uint32_t u = blockIdx.x * WAVE + threadIdx.x;
   if (u >= b.n_umsg || (b.mflags[u] & MF_H_INF)) return;
@@ -91,6 +140,14 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc(PipelineBuffers b) {
   const uint32_t c = blockIdx.x * WAVE + threadIdx.x;
   if (c >= b.n_chunks) return;
   const uint32_t k0 = b.chunk_first[c], k1 = b.chunk_first[c + 1];
+#if ACC_PREFETCH
+  __shared__ uint32_t pre[W_LINE * WAVE];
+  auto msg_of = [&](uint32_t k) {
+    const uint32_t i = b.chunk_items[k];
+    return UNITS ? b.unit_msg[i] : b.msg_idx[i];
+  };
+  if (k1 > k0) line_prefetch(pre, b.lines, b.nm, msg_of(k0));
+#endif
   fp12 f = fp12_one();
   int bit = 62;
   bool add_next = false;
@@ -116,12 +173,28 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc(PipelineBuffers b) {
         m = b.msg_idx[i];
         active = b.include[i] != 0;
       }
+#if ACC_PREFETCH
+      // this item's line (fetched into the slot one item ahead), then the slot takes the next one
+      line_wait();
+      line3 L;
+      L.l0 = ld_fp2_pre(pre, 0);
+      L.c1 = ld_fp2_pre(pre, 2 * W_FP);
+      L.c4 = ld_fp2_pre(pre, 4 * W_FP);
+      line_read_done();
+      if (k + 1 < k1)
+        line_prefetch(pre, o, b.nm, msg_of(k + 1));
+      else if (s + 1 < MILLER_STEPS)
+        line_prefetch(pre, o + (size_t)W_LINE * b.nm, b.nm, msg_of(k0));
+      if (!active || (b.mflags[m] & MF_H_INF)) continue;
+      const g1a P = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
+#else
       if (!active || (b.mflags[m] & MF_H_INF)) continue;
       const g1a P = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
       line3 L;
       L.l0 = ld_fp2(o, b.nm, m, 0);
       L.c1 = ld_fp2(o, b.nm, m, 2 * W_FP);
       L.c4 = ld_fp2(o, b.nm, m, 4 * W_FP);
+#endif
 #if BLS_LINE_PAIRS
       const fp2 l1 = fp2_mul_fp(L.c1, P.x), l4 = fp2_mul_fp(L.c4, P.y);
       if (pend) {
@@ -164,6 +237,14 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc2(PipelineBuffers b) {
   const uint32_t c = q >> 1, h = q & 1;  // both lanes of a pair see the same c (WAVE is even)
   if (c >= b.n_chunks) return;           // whole pairs leave together: the exchanges below stay within live pairs
   const uint32_t k0 = b.chunk_first[c], k1 = b.chunk_first[c + 1];
+#if ACC_PREFETCH
+  __shared__ uint32_t pre[W_LINE * WAVE];
+  auto msg_of = [&](uint32_t k) {
+    const uint32_t i = b.chunk_items[k];
+    return UNITS ? b.unit_msg[i] : b.msg_idx[i];
+  };
+  if (k1 > k0) line_prefetch(pre, b.lines, b.nm, msg_of(k0));
+#endif
   fp6 mine = h ? fp6_zero() : fp6_one();
   int bit = 62;
   bool add_next = false;
@@ -229,11 +310,25 @@ STAGE_KERNEL_W(BLSGPU_WPE_ACC) void k_miller_acc2(PipelineBuffers b) {
         m = b.msg_idx[i];
         active = b.include[i] != 0;
       }
+#if ACC_PREFETCH
+      line_wait();
+      fp2 l0 = ld_fp2_pre(pre, 0), l1 = ld_fp2_pre(pre, 2 * W_FP), l4 = ld_fp2_pre(pre, 4 * W_FP);
+      line_read_done();
+      if (k + 1 < k1)
+        line_prefetch(pre, o, b.nm, msg_of(k + 1));
+      else if (s + 1 < MILLER_STEPS)
+        line_prefetch(pre, o + (size_t)W_LINE * b.nm, b.nm, msg_of(k0));
+      if (!active || (b.mflags[m] & MF_H_INF)) continue;  // the same on both lanes of the pair
+      const g1a P = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
+      l1 = fp2_mul_fp(l1, P.x);
+      l4 = fp2_mul_fp(l4, P.y);
+#else
       if (!active || (b.mflags[m] & MF_H_INF)) continue;  // the same on both lanes of the pair
       const g1a P = ld_g1a(UNITS ? b.unit_p : b.pk_aff, b.n, i);
       const fp2 l0 = ld_fp2(o, b.nm, m, 0);
       const fp2 l1 = fp2_mul_fp(ld_fp2(o, b.nm, m, 2 * W_FP), P.x);
       const fp2 l4 = fp2_mul_fp(ld_fp2(o, b.nm, m, 4 * W_FP), P.y);
+#endif
 #if BLS_ACC2_PAIRS
       if (!pend) {
         q0 = l0;
