@@ -198,7 +198,9 @@ struct Device {
   // pairs, taking urgent calls from uqueue (under q_mu) one at a time.  It never counts in runs_inflight and never takes
   // enq_mu, so an urgent call waits for no throughput run on the host; on the device its streams either run on a
   // reserved CU partition that the pipeline streams are masked off ("urgent_cus" > 0) or at the highest priority.
-  hipStream_t ust[4] = {};
+  hipStream_t ust[4] = {};         // the urgent lane's streams, created by its dispatcher before its first run
+  std::vector<uint32_t> umask;      // their CU mask (empty: plain streams of priority uprio)
+  int uprio = 0;
   std::deque<Task> uqueue;
   Slot* uslot = nullptr;
   std::thread uworker;
@@ -1909,6 +1911,7 @@ void worker_loop(Device* d, Slot* sl) {
 // (multithread/index.ts:138-151).  `alone` holds for its streams, so a run takes the latency forms of an idle device:
 // the speculative MSM and the pubkey branch on the idle pair, r_i sig_i beside the batch pass, cooperative fallback
 // checks.  Exits when the device stops and its urgent queue is drained.
+bool ensure_urgent_streams(Device* d, Slot* sl);
 void urgent_loop(Device* d, Slot* sl) {
   tl_dispatcher = true;
   pthread_setname_np(pthread_self(), "blsgpu-urgent");
@@ -1953,6 +1956,18 @@ void urgent_loop(Device* d, Slot* sl) {
     tl_run_t0 = std::chrono::steady_clock::now();
     tl_merge_ms = 0;
     const size_t np = parts.size();
+    if (!ensure_urgent_streams(d, sl)) {  // no streams: every call of the run completes with a device error
+      for (size_t p = 0; p < np; p++) {
+        Call* c = parts[p].call;
+        const Shard& sh = c->shards[parts[p].shard];
+        for (uint32_t j = sh.job_begin; j < sh.job_end; j++) c->job_result[j] = -BLSGPU_DEVICE_ERROR;
+        c->rc[parts[p].shard] = BLSGPU_DEVICE_ERROR;
+        c->sst[parts[p].shard].urgent_lane = 1;
+        if (c->remaining.fetch_sub(1) == 1) finish_call(c);
+      }
+      d->upending.fetch_sub((int)np, std::memory_order_relaxed);
+      continue;
+    }
     if (np == 1) {
       run_task(*d, *sl, parts[0]);  // completes the call
     } else {
@@ -2049,7 +2064,31 @@ void create_streams(blsgpu_ctx* ctx, Device* d) {
     const bool high = ctx->pipeline_prio && ((BLSGPU_STREAM_PRIO & (1 << (k & 3))) != 0 || (k >= kStreams && (k & 1)));
     d->st[k] = make_stream(d->main_mask, high ? prio_hi : prio_lo);
   }
-  for (int k = 0; k < 4; k++) d->ust[k] = make_stream(pmask, prio_hi);
+  // The urgent streams are created when the lane takes its first call (ensure_urgent_streams): a process that never
+  // verifies an urgent call holds no idle hardware queues for them (each CU-masked stream is a queue of its own, and
+  // eight device contexts on one GPU -- bench.py --devices-same -- would otherwise hold 32).  BLSGPU_URGENT_EAGER=1
+  // (build define) creates them here.
+  d->umask = pmask;
+  d->uprio = prio_hi;
+#if BLSGPU_URGENT_EAGER
+  for (int k = 0; k < 4; k++) d->ust[k] = make_stream(d->umask, d->uprio);
+#endif
+}
+
+// The urgent lane's streams on first use (its dispatcher thread; the slot's buffers follow stream 0).  A failed
+// creation leaves them null and is reported as a device error for the run.
+bool ensure_urgent_streams(Device* d, Slot* sl) {
+  if (d->ust[0]) return true;
+  try {
+    HIPCHK(hipSetDevice(d->id));
+    for (int k = 0; k < 4; k++) d->ust[k] = make_stream(d->umask, d->uprio);
+  } catch (HipError&) {
+    for (hipStream_t& st : d->ust)
+      if (st) (void)hipStreamDestroy(st), st = nullptr;
+    return false;
+  }
+  sl->set_stream(d->ust[0]);
+  return true;
 }
 
 // A slot's events: the two its dispatcher waits on (join_msg, done) block the thread in the driver when
