@@ -205,6 +205,9 @@ struct Device {
   Slot* uslot = nullptr;
   std::thread uworker;
   std::atomic<int> upending{0};  // urgent calls queued or running here (routing of urgent calls)
+  // batch groups whose equation failed although every job of theirs verified on its own in the fallback -- zero unless a
+  // kernel computed a group's equation wrong (read-only option "spurious_groups"; each one is also logged)
+  std::atomic<uint64_t> spurious_groups{0};
   int urgent_cus = 0;            // CUs of the partition the streams were created with (0 = none)
   std::vector<uint32_t> main_mask;  // CU mask of the pipeline and fallback streams (empty = all CUs, priorities)
   bool blocking_sync = true;        // the dispatchers' wait events block instead of spinning (create_slot_events)
@@ -498,11 +501,14 @@ struct MsgIndex {
 
 // Batch-group size for a run (group_adapt).  A group costs a fixed ~14.7k Montgomery multiplications (its
 // MillerLoop(-g1, S) 5,747, final exponentiation 7,835, MSM range 1,085; lodestar_amd/op_counts.json), and when it fails
-// every clean job in it is re-checked: per set ~13.6k / (sets per job) + 1.3k (the job's own S_j, MillerLoop(-g1, S_j)
-// and final exponentiation; the per-set Miller values are reused).  With invalid sets at rate f a group of g sets fails
-// with probability 1 - (1 - f)^g, so the expected cost per set is 14.7k / g + (1 - (1 - f)^g) * retry: the size that
-// minimises it over powers of two in [8, group_sets].  All valid (f = 0): group_sets (1,024); the reference pool's 1%
-// invalid gossip (C5, jobs of 1-3 sets): ~16.  Per-job results do not depend on the grouping (each job's verdict is its
+// every clean job in it is re-checked: per set 1.3k (the set's r_i sig_i; its Miller value is reused) plus its job's
+// share of a sub-group check, ~13.6k per 16 jobs (the fallback's level 1, one final exponentiation per kFbSub jobs;
+// only failing sub-groups check job by job).  With invalid sets at rate f a group of g sets fails with probability
+// 1 - (1 - f)^g, so the expected cost per set is 14.7k / g + (1 - (1 - f)^g) * retry: the size that minimises it over
+// powers of two in [8, group_sets].  All valid (f = 0): group_sets (1,024); the reference pool's 1% invalid gossip
+// (C5, jobs of 1-3 sets): 32.  C5 by fixed group size (profiles/r06_c5_groups.json): 16 sets 721-797k sets/s, 32
+// 753-830k, 64 795-809k, 128 706-724k, 1,024 617-739k; the first form of this model (retry priced at one final
+// exponentiation per job) chose 16: 693k.  Per-job results do not depend on the grouping (each job's verdict is its
 // own, as the reference's per-job re-verification); only the work does.
 uint32_t adapt_group_sets(Device& d, int64_t group_sets, double sets_per_job) {
   double f;
@@ -512,7 +518,7 @@ uint32_t adapt_group_sets(Device& d, int64_t group_sets, double sets_per_job) {
   }
   const uint32_t gmax = (uint32_t)std::max<int64_t>(1, group_sets);
   if (f <= 0 || gmax <= 8) return gmax;
-  const double retry = 13600.0 / std::max(1.0, sets_per_job) + 1300.0, fixed = 14700.0;
+  const double retry = 13600.0 / (16.0 * std::max(1.0, sets_per_job)) + 1300.0, fixed = 14700.0;
   uint32_t best = gmax;
   double best_c = fixed / gmax + (1.0 - std::pow(1.0 - f, (double)gmax)) * retry;
   for (uint32_t g = 8; g < gmax; g *= 2) {
@@ -1145,6 +1151,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     jr[j] = err ? -err : 2;  // 2 = pending
   }
   std::vector<uint32_t> retry;  // clean jobs of failed groups, each re-checked on its own
+  std::vector<uint32_t> failed_g;  // groups whose own equation failed (their clean jobs are in retry)
   for (uint32_t g = 0; g < ng0; g++) {
     std::vector<uint32_t> clean;
     bool dropped = false;  // a rejected job of the group has sets (they may sit in a speculative S_g)
@@ -1173,13 +1180,15 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       }
     }
     if (clean.empty()) continue;
+    // A failed group's clean jobs are re-verified one by one, also when the group held a single clean job (its
+    // equation was that job's own): the reference re-verifies every job of a failed chunk whatever its size
+    // (worker.ts:76-98), so a job's false is always its own check's answer, never only its group's.
     if (plan) {
       if (sl.h_res.p[o_ok + g]) {
         for (uint32_t j : clean) jr[j] = 1;
-      } else if (clean.size() == 1) {
-        jr[clean[0]] = 0;
       } else {
         retry.insert(retry.end(), clean.begin(), clean.end());
+        failed_g.push_back(g);
       }
       continue;
     }
@@ -1187,11 +1196,10 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       for (uint32_t j : clean) jr[j] = 1;
       if (group_jobs[g].second - group_jobs[g].first > 1)
         for (uint32_t j : clean) st.batch_sigs_success += job_sets(j).second - job_sets(j).first;
-    } else if (clean.size() == 1) {  // the group's equation was this job's own
-      jr[clean[0]] = 0;
     } else {
       if (clean.size() > 1) st.batch_retries++;
       retry.insert(retry.end(), clean.begin(), clean.end());
+      failed_g.push_back(g);
     }
   }
 
@@ -1358,6 +1366,19 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       HIPCHK(hipEventRecord(sl.done, sfb));
       HIPCHK(hipEventSynchronize(sl.done));
       for (uint32_t k = 0; k < ns; k++) jr[retry[sel[k]]] = sl.h_ok.p[k] ? 1 : 0;
+    }
+  }
+  // a failed group whose clean jobs all verify on their own: its batch equation was computed wrong (the random
+  // combination of valid sets always holds)
+  for (uint32_t g : failed_g) {
+    bool all_ok = true;
+    for (uint32_t j = group_jobs[g].first; j < group_jobs[g].second && all_ok; j++)
+      if (jr[j] != 1 && jr[j] >= 0) all_ok = false;  // errors (negative) are not in the equation
+    if (all_ok) {
+      d.spurious_groups.fetch_add(1, std::memory_order_relaxed);
+      fprintf(stderr, "[blsgpu] device %d: batch group %u (jobs %u-%u) of a %u-set run failed its equation while "
+              "every job verifies on its own (spec %d, merged %d, coop %d, mk %u)\n", d.id, g, group_jobs[g].first,
+              group_jobs[g].second - 1, n, (int)spec, (int)merged, (int)coop, mk);
     }
   }
   for (uint32_t j = 0; j < nj; j++) job_result[sh.job_begin + j] = (int8_t)jr[j];
@@ -2640,6 +2661,12 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   }
   if (k == "abi_version") {
     *value = BLSGPU_ABI_VERSION;
+    return BLSGPU_OK;
+  }
+  if (k == "spurious_groups") {
+    uint64_t c = 0;
+    for (const Device* d : ctx->devs) c += d->spurious_groups.load(std::memory_order_relaxed);
+    *value = (int64_t)c;
     return BLSGPU_OK;
   }
   std::lock_guard<std::mutex> lk(ctx->opt_mu);
