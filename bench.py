@@ -619,7 +619,9 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--devices-same", type=int, default=-1,
                     help="host-capacity mode: the --gpus N in-process device contexts all on this one device (N "
-                         "dispatcher sets and stream sets on one GPU; throughput is one GPU's, the host cost is N's)")
+                         "dispatcher sets and stream sets on one GPU; throughput is one GPU's, the host cost is N's); "
+                         "under torch.distributed.run every rank on this device (the multi-process path rehearsed on "
+                         "one GPU)")
     ap.add_argument("--urgent-every-ms", type=float, default=0.0,
                     help="latency probe: during the timed region one thread submits urgent 1- / 3-set calls "
                          "(verifyOnMainThread, BLSGPU_JOB_URGENT) this often, and their isolated latency is measured "
@@ -644,8 +646,8 @@ def main():
     # (each call sharded over them by the runtime)
     n_dev = args.gpus if world == 1 else 1
     devices = list(range(n_dev)) if world == 1 else [local_rank]
-    if args.devices_same >= 0 and world == 1:
-        devices = [args.devices_same] * n_dev
+    if args.devices_same >= 0:  # rehearsal on fewer GPUs: every in-process device / every rank on this one
+        devices = [args.devices_same] * len(devices)
     ctx = Context(devices)
     ctx.set_option("group_sets", args.group_sets)
     ctx.set_option("group_policy", args.group_policy)
@@ -699,8 +701,9 @@ def main():
         lat_ms = (time.perf_counter() - t1) * 1e3
         if not np.array_equal(res, expected):
             bad = np.nonzero(res != expected)[0]
+            fields = {k: (list(getattr(st, k)) if k == "stage_ms" else getattr(st, k)) for k, _ in st._fields_}
             raise SystemExit(f"verification mismatch on {len(bad)} jobs (first {bad[:8]}: got {res[bad[:8]]}, "
-                             f"want {expected[bad[:8]]})")
+                             f"want {expected[bad[:8]]}); call {i}, variant {i % n_var}, run stats {fields}")
         return st, lat_ms
 
     pool = ThreadPoolExecutor(max_workers=max(1, args.inflight, 4 * ctx.get_option("slots") + 4))
@@ -764,6 +767,9 @@ def main():
     w1 = time.monotonic_ns()
     ctx.set_option("profile", 0)
     stats = [r[0] for r in results]
+    # re-checked jobs over the timed calls (a run's count is reported to each of its calls): 0 for an all-valid
+    # workload unless a batch group's equation failed for valid sets
+    fallback_jobs_timed = int(sum(s.fallback_jobs for s in stats))
     call_lat = np.array([r[1] for r in results])
     from lodestar_amd.shard import max_over_ranks
 
@@ -802,6 +808,8 @@ def main():
                        pipeline_runs_timed=len(runs_timed),
                        parallelism=f"shard-by-job x{n_gpus} ({'one process per GPU' if world > 1 else 'in-process devices'}), no collective"),
         "p50_batch_latency_ms": round(float(np.median(lat)), 3),
+        "fallback_jobs_timed": fallback_jobs_timed,
+        "spurious_groups": ctx.get_option("spurious_groups"),
         # host cost of the timed region: CPU seconds of the whole process per million sets verified, and each run's
         # host time from its slot taking it to its input copy (blsgpu_stats.host_ms)
         "host": {"cpu_s_per_million_sets": round(cpu_s / (total_sets / 1e6), 4), "process_cpu_s": round(cpu_s, 3),
