@@ -223,7 +223,9 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
 int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value);
 /* Current value of a tunable (the keys of blsgpu_set_option; "slots" = the slots device 0 runs, or will create
  * on the first call) or of a read-only property: "hw_queues" (the GPU_MAX_HW_QUEUES HIP runs with),
- * "abi_version". */
+ * "abi_version", "spurious_groups" (batch groups whose equation failed although every job of theirs verified on its
+ * own in the fallback, over the context's life: zero unless a kernel computed a group's equation wrong; each is also
+ * logged to stderr). */
 int blsgpu_get_option(const blsgpu_ctx* ctx, const char* key, int64_t* value);
 
 /* chunkifyMaximizeChunkSize(arr of len items, min_per_chunk) (multithread/utils.ts:4-19): writes the first

@@ -58,3 +58,6 @@ def test_unknown_and_read_only_keys(ctx):
         assert v > 0
         with pytest.raises(ValueError):
             ctx.set_option(ro, v + 1)
+    assert ctx.get_option("spurious_groups") == 0
+    with pytest.raises(ValueError):
+        ctx.set_option("spurious_groups", 1)

@@ -22,7 +22,7 @@ def test_every_option_documented():
     integration = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     assert sorted(k for k in set_keys if f'"{k}"' not in header) == []
     assert sorted(k for k in set_keys if f"`{k}`" not in integration) == []
-    assert get_keys - set_keys == {"hw_queues", "abi_version"}
+    assert get_keys - set_keys == {"hw_queues", "abi_version", "spurious_groups"}
     assert set_keys <= get_keys
 
 

@@ -35,7 +35,7 @@ struct acc2 {
     return t[0] + t[1] + carry;
   }
 };
-template <int KIND>  // 0 mul, 1 sqr, 2 dot
+template <int KIND, bool GATE>  // KIND 0 mul, 1 sqr, 2 dot; GATE: column k's chains start after column k-2's carry
 BLS_INL fp split_body(const fp& x1, const fp& y1, const fp& x2, const fp& y2) {
   fp r;
   uint32_t m[BLS_NL], a2[BLS_NL];
@@ -44,10 +44,14 @@ BLS_INL fp split_body(const fp& x1, const fp& y1, const fp& x2, const fp& y2) {
     for (int i = 0; i < BLS_NL; i++) a2[i] = x1.l[i] << 1;
   }
   uint64_t carry = 0;
+  uint32_t gate[2 * BLS_NL];
 #pragma unroll
   for (int k = 0; k < 2 * BLS_NL - 1; k++) {
     const int lo = k < BLS_NL ? 0 : k - BLS_NL + 1, hi = k < BLS_NL ? k : BLS_NL - 1;
     acc2 t;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (GATE && k >= 2) asm("" : "+v"(t.t[0]), "+v"(t.t[1]) : "v"(gate[k - 2]));
+#endif
     if (KIND == 1) {
 #pragma unroll
       for (int i = lo; 2 * i < k; i++) t.mad(a2[i], x1.l[k - i]);
@@ -72,39 +76,37 @@ BLS_INL fp split_body(const fp& x1, const fp& y1, const fp& x2, const fp& y2) {
       r.l[k - BLS_NL] = (uint32_t)acc & BLS_MASK;
     }
     carry = acc >> BLS_LB;
+    gate[k] = (uint32_t)carry;
   }
   r.l[BLS_NL - 1] = (uint32_t)carry;
   return r;
 }
-BLS_INL fp mul_split(const fp& a, const fp& b) { return split_body<0>(a, b, a, b); }
-BLS_INL fp sqr_split(const fp& a) { return split_body<1>(a, a, a, a); }
-BLS_INL fp dot_split(const fp& x1, const fp& y1, const fp& x2, const fp& y2) { return split_body<2>(x1, y1, x2, y2); }
 
 #if defined(__HIP_DEVICE_COMPILE__)
 // ---- register-ABI wrappers: V = 0 cur, 1 split ----
-#define RET14(r)                                       \
-  fp_ret o;                                            \
-  for (int i = 0; i < BLS_NL; i++) o.l[i] = (r).l[i]; \
-  return o;
-__device__ __noinline__ fp_ret mul_cur_r(BLS_PARAMS14(a), BLS_PARAMS14(b)) {
+#define RET14(r)                                         \
+  {                                                      \
+    const fp r_ = r;                                     \
+    fp_ret o;                                            \
+    for (int i = 0; i < BLS_NL; i++) o.l[i] = r_.l[i]; \
+    return o;                                            \
+  }
+template <int V>
+__device__ __noinline__ fp_ret mul_r(BLS_PARAMS14(a), BLS_PARAMS14(b)) {
   const fp x = BLS_INIT14(a), y = BLS_INIT14(b);
-  RET14(fp_mul_body(x, y))
+  if (V == 0) { RET14(fp_mul_body(x, y)) }
+  RET14((split_body<0, V == 2>(x, y, x, y)))
 }
-__device__ __noinline__ fp_ret mul_split_r(BLS_PARAMS14(a), BLS_PARAMS14(b)) {
-  const fp x = BLS_INIT14(a), y = BLS_INIT14(b);
-  RET14(mul_split(x, y))
-}
-__device__ __noinline__ fp_ret sqr_cur_r(BLS_PARAMS14(a)) {
+template <int V>
+__device__ __noinline__ fp_ret sqr_r(BLS_PARAMS14(a)) {
   const fp x = BLS_INIT14(a);
-  RET14(fp_sqr_body(x))
-}
-__device__ __noinline__ fp_ret sqr_split_r(BLS_PARAMS14(a)) {
-  const fp x = BLS_INIT14(a);
-  RET14(sqr_split(x))
+  if (V == 0) { RET14(fp_sqr_body(x)) }
+  RET14((split_body<1, V == 2>(x, x, x, x)))
 }
 // the lane-pair product: this lane's coefficient (fp2x_mul_body's operand setup, then the dot product)
 template <int V>
-BLS_INL fp pair_body(const fp& a, const fp& b) {
+__device__ __noinline__ fp_ret pair_r(BLS_PARAMS14(a_), BLS_PARAMS14(b_)) {
+  const fp a = BLS_INIT14(a_), b = BLS_INIT14(b_);
   const bool odd = fp2x_k() != 0;
   fp pa, b0, y;
 #pragma unroll
@@ -114,23 +116,16 @@ BLS_INL fp pair_body(const fp& a, const fp& b) {
     const uint32_t b1 = dpp_odd(b.l[i]);
     y.l[i] = odd ? b1 : FP_16P_K.l[i] - b1;
   }
-  return V ? dot_split(a, b0, pa, y) : fp_dot_body(a, b0, pa, y);
-}
-__device__ __noinline__ fp_ret pair_cur_r(BLS_PARAMS14(a), BLS_PARAMS14(b)) {
-  const fp x = BLS_INIT14(a), y = BLS_INIT14(b);
-  RET14(pair_body<0>(x, y))
-}
-__device__ __noinline__ fp_ret pair_split_r(BLS_PARAMS14(a), BLS_PARAMS14(b)) {
-  const fp x = BLS_INIT14(a), y = BLS_INIT14(b);
-  RET14(pair_body<1>(x, y))
+  if (V == 0) { RET14(fp_dot_body(a, b0, pa, y)) }
+  RET14((split_body<2, V == 2>(a, b0, pa, y)))
 }
 
 template <int OP, int V>
 __device__ __forceinline__ fp call(const fp& a, const fp& b) {
   fp_ret t;
-  if (OP == 0) t = V ? mul_split_r(BLS_ARGS14(a), BLS_ARGS14(b)) : mul_cur_r(BLS_ARGS14(a), BLS_ARGS14(b));
-  if (OP == 1) t = V ? sqr_split_r(BLS_ARGS14(a)) : sqr_cur_r(BLS_ARGS14(a));
-  if (OP == 2) t = V ? pair_split_r(BLS_ARGS14(a), BLS_ARGS14(b)) : pair_cur_r(BLS_ARGS14(a), BLS_ARGS14(b));
+  if (OP == 0) t = mul_r<V>(BLS_ARGS14(a), BLS_ARGS14(b));
+  if (OP == 1) t = sqr_r<V>(BLS_ARGS14(a));
+  if (OP == 2) t = pair_r<V>(BLS_ARGS14(a), BLS_ARGS14(b));
   fp r;
   for (int i = 0; i < BLS_NL; i++) r.l[i] = t.l[i];
   return r;
@@ -176,10 +171,10 @@ int main() {
   CHECK(hipMalloc(&d1, words * 4));
   uint32_t* h0 = (uint32_t*)malloc(words * 4);
   uint32_t* h1 = (uint32_t*)malloc(words * 4);
-  struct { const char* name; kfn cur, split; } ks[] = {
-      {"fp_mul", k_chain<0, 0>, k_chain<0, 1>},
-      {"fp_sqr", k_chain<1, 0>, k_chain<1, 1>},
-      {"fp2x_mul (lane pair)", k_chain<2, 0>, k_chain<2, 1>},
+  struct { const char* name; kfn v[3]; } ks[] = {
+      {"fp_mul", {k_chain<0, 0>, k_chain<0, 1>, k_chain<0, 2>}},
+      {"fp_sqr", {k_chain<1, 0>, k_chain<1, 1>, k_chain<1, 2>}},
+      {"fp2x_mul (lane pair)", {k_chain<2, 0>, k_chain<2, 1>, k_chain<2, 2>}},
   };
   printf("{\"device\": \"%s\", \"simds\": %d, \"calls_per_lane\": %d, \"results\": [\n", prop.gcnArchName, simds,
          2 * ITERS);
@@ -187,9 +182,10 @@ int main() {
   for (auto& k : ks) {
     for (int wps : {1, 2, 4}) {
       const int grid = simds * wps;
-      float ms[2];
-      for (int v = 0; v < 2; v++) {
-        kfn f = v ? k.split : k.cur;
+      float ms[3];
+      size_t diff[3] = {0, 0, 0};
+      for (int v = 0; v < 3; v++) {
+        kfn f = k.v[v];
         uint32_t* d = v ? d1 : d0;
         hipLaunchKernelGGL(f, dim3(grid), dim3(64), 0, 0, d, 1u, ITERS);
         CHECK(hipDeviceSynchronize());
@@ -203,17 +199,16 @@ int main() {
         CHECK(hipEventSynchronize(e1));
         CHECK(hipEventElapsedTime(&ms[v], e0, e1));
         ms[v] /= reps;
+        const size_t n = (size_t)grid * 64 * 2 * BLS_NL;
+        CHECK(hipMemcpy(v ? h1 : h0, d, n * 4, hipMemcpyDeviceToHost));
+        if (v)
+          for (size_t i = 0; i < n; i++) diff[v] += h0[i] != h1[i];
       }
-      const size_t n = (size_t)grid * 64 * 2 * BLS_NL;
-      CHECK(hipMemcpy(h0, d0, n * 4, hipMemcpyDeviceToHost));
-      CHECK(hipMemcpy(h1, d1, n * 4, hipMemcpyDeviceToHost));
-      size_t diff = 0;
-      for (size_t i = 0; i < n; i++) diff += h0[i] != h1[i];
       const double calls = 2.0 * ITERS * grid * 64;
-      printf("%s  {\"op\": \"%s\", \"waves_per_simd\": %d, \"cur_ms\": %.3f, \"split_ms\": %.3f, \"speedup\": %.3f, "
-             "\"cur_products_per_s\": %.4e, \"split_products_per_s\": %.4e, \"limb_mismatches\": %zu}",
-             first ? "" : ",\n", k.name, wps, ms[0], ms[1], ms[0] / ms[1], calls / (ms[0] * 1e-3),
-             calls / (ms[1] * 1e-3), diff);
+      printf("%s  {\"op\": \"%s\", \"waves_per_simd\": %d, \"ms\": {\"cur\": %.3f, \"split\": %.3f, \"gated\": %.3f}, "
+             "\"products_per_s\": {\"cur\": %.4e, \"split\": %.4e, \"gated\": %.4e}, \"limb_mismatches\": [%zu, %zu]}",
+             first ? "" : ",\n", k.name, wps, ms[0], ms[1], ms[2], calls / (ms[0] * 1e-3), calls / (ms[1] * 1e-3),
+             calls / (ms[2] * 1e-3), diff[1], diff[2]);
       first = false;
     }
   }
