@@ -60,6 +60,16 @@ struct HipError {
 // growths of stream-ordered slot buffers by this thread (run_shard: an input copy may leave the run's stream only when
 // no buffer of the run was (re)allocated in that stream's order)
 thread_local uint64_t tl_async_grow = 0;
+// Diagnostics (BLSGPU_POISON=1 in the environment): every (re)allocated device buffer is filled with 0xA5 bytes before
+// first use, so a kernel that reads memory no kernel of its run wrote fails every time instead of only when the
+// allocator hands it memory another run left with different contents.
+inline bool poison_buffers() {
+  static const bool on = [] {
+    const char* v = getenv("BLSGPU_POISON");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
 template <class T>
 struct DevBuf {
   T* p = nullptr;
@@ -72,11 +82,16 @@ struct DevBuf {
       if (p) HIPCHK(hipFreeAsync(p, st));
       p = nullptr;
       HIPCHK(hipMallocAsync((void**)&p, c * sizeof(T), st));
+      if (poison_buffers()) HIPCHK(hipMemsetAsync(p, 0xA5, c * sizeof(T), st));
       tl_async_grow++;
     } else {
       if (p) HIPCHK(hipFree(p));
       p = nullptr;
       HIPCHK(hipMalloc((void**)&p, c * sizeof(T)));
+      if (poison_buffers()) {  // the fill is on the null stream: complete it before any stream uses the buffer
+        HIPCHK(hipMemset(p, 0xA5, c * sizeof(T)));
+        HIPCHK(hipStreamSynchronize(nullptr));
+      }
     }
     cap = c;
   }
@@ -97,6 +112,7 @@ struct HostBuf {  // pinned staging
     p = nullptr;
     size_t c = std::max<size_t>(n, cap * 2);
     HIPCHK(hipHostMalloc((void**)&p, c * sizeof(T), hipHostMallocDefault));
+    if (poison_buffers()) memset(p, 0x5A, c * sizeof(T));
     cap = c;
   }
   void release() {

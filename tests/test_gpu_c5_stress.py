@@ -92,3 +92,37 @@ def test_c5_many_calls_under_load(env, adapt):
             json.dump(info, fh, indent=1, default=str)
         pytest.fail(f"C5 mismatch: {json.dumps(info, default=str)[:2000]}")
     assert spurious == 0, f"{spurious} batch groups failed although all their jobs verify (see stderr)"
+
+
+COLD = int(os.environ.get("C5_COLD_ROUNDS", "4"))
+
+
+def test_c5_cold_contexts():
+    """The bench's cold start, COLD times: a fresh context, the C5 workload and its message variants signed on the
+    device, one round of 32 calls in flight.  On a mismatch the job's sets go through the CPU oracle with the
+    device-made signatures: oracle false = the device SIGNER made a wrong signature (a test-input fault, not a
+    verifier one); oracle true = the verifier answered wrong."""
+    from lodestar_amd.native import Context
+
+    strip = lambda x: {k: v for k, v in x.items() if not k.startswith("_")}
+    for it in range(COLD):
+        ctx = Context([0])
+        try:
+            w, n, desc, _ = bench.build_workload(ctx, "C5", 0)
+            expected = w.pop("expected")
+            calls = [strip(bench.message_variant(ctx, w, v)) for v in range(32)]
+            with ThreadPoolExecutor(max_workers=32) as pool:
+                res = list(pool.map(lambda v: ctx.verify_raw(**calls[v], seed=bench.SEED), range(32)))
+            for v, (got, st) in enumerate(res):
+                if not np.array_equal(got, expected):
+                    info = diagnose(ctx, w, calls[v], expected, got, st, v)
+                    info.update(cold_iteration=it)
+                    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+                    with open(os.path.join(ROOT, "gpurun_out", "c5_cold_fail.json"), "w") as fh:
+                        json.dump(info, fh, indent=1, default=str)
+                    signer = all(r["oracle_job"] == r["got"] for r in info["jobs"])
+                    pytest.fail(("device SIGNER fault" if signer else "VERIFIER fault") +
+                                f": {json.dumps(info, default=str)[:2000]}")
+            assert ctx.get_option("spurious_groups") == 0
+        finally:
+            ctx.close()
