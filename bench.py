@@ -702,8 +702,12 @@ def main():
         if not np.array_equal(res, expected):
             bad = np.nonzero(res != expected)[0]
             fields = {k: (list(getattr(st, k)) if k == "stage_ms" else getattr(st, k)) for k, _ in st._fields_}
+            # the same call again: the same wrong jobs = wrong inputs (a device-made signature), else a transient
+            res2, _ = ctx.verify_raw(**calls[i % n_var], seed=SEED)
+            bad2 = np.nonzero(res2 != expected)[0]
             raise SystemExit(f"verification mismatch on {len(bad)} jobs (first {bad[:8]}: got {res[bad[:8]]}, "
-                             f"want {expected[bad[:8]]}); call {i}, variant {i % n_var}, run stats {fields}")
+                             f"want {expected[bad[:8]]}); call {i}, variant {i % n_var}, run stats {fields}; "
+                             f"re-verified: {len(bad2)} mismatches, same jobs {np.array_equal(bad, bad2)}")
         return st, lat_ms
 
     pool = ThreadPoolExecutor(max_workers=max(1, args.inflight, 4 * ctx.get_option("slots") + 4))

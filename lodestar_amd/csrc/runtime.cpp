@@ -70,6 +70,15 @@ inline bool poison_buffers() {
   }();
   return on;
 }
+// Diagnostics (BLSGPU_SYNC_GROW=1): buffer growth with a whole-device synchronisation and plain hipFree / hipMalloc
+// instead of stream-ordered hipFreeAsync / hipMallocAsync.
+inline bool sync_grow() {
+  static const bool on = [] {
+    const char* v = getenv("BLSGPU_SYNC_GROW");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
 template <class T>
 struct DevBuf {
   T* p = nullptr;
@@ -78,7 +87,15 @@ struct DevBuf {
   void ensure(size_t n) {
     if (n <= cap) return;
     const size_t c = std::max<size_t>(n, cap * 2);
-    if (st) {
+    if (st && sync_grow()) {
+      HIPCHK(hipDeviceSynchronize());
+      if (p) HIPCHK(hipFree(p));
+      p = nullptr;
+      HIPCHK(hipMalloc((void**)&p, c * sizeof(T)));
+      if (poison_buffers()) HIPCHK(hipMemset(p, 0xA5, c * sizeof(T)));
+      HIPCHK(hipDeviceSynchronize());
+      tl_async_grow++;
+    } else if (st) {
       if (p) HIPCHK(hipFreeAsync(p, st));
       p = nullptr;
       HIPCHK(hipMallocAsync((void**)&p, c * sizeof(T), st));

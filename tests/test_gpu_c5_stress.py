@@ -21,7 +21,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 THREADS = bench.host_cpus()["threads"]
 ROUNDS = int(os.environ.get("C5_STRESS_ROUNDS", "48"))
-VARIANTS = 8
+# one message variant per call in flight (+1), as bench.py: merged runs share no signing root, so the runs keep their
+# per-set Miller values for the fallback (runtime keep_f) -- with fewer variants merged calls share roots and pair by
+# units instead
+VARIANTS = int(os.environ.get("C5_STRESS_VARIANTS", "33"))
 
 
 @pytest.fixture(scope="module")
@@ -60,6 +63,7 @@ def diagnose(ctx, w, call, expected, got, st, v):
 
 @pytest.mark.parametrize("adapt", [1, 0])
 def test_c5_many_calls_under_load(env, adapt):
+    """ROUNDS rounds of 32 calls in flight (the calls of a round cycle through the variants)."""
     ctx, w, calls, expected = env
     old = ctx.get_option("group_adapt")
     ctx.set_option("group_adapt", adapt)
