@@ -198,7 +198,9 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
  * parallel pubkey branch and r_i sig_i, cooperative fallback checks; default 4096), "fb_direct_min" (large runs under
  * load with >= this many retried jobs check each one directly, default 1024, 0 = never), "fb_check6" (those checks: 0
  * one lane each, 1 Miller loop on one lane and the final exponentiation on six, 2 both on six lanes; default 2),
- * "fb_force_busy" (tests: every run's fallback takes the under-load forms, 0/1, default 0), "early_release" /
+ * "fb_force_busy" (tests: every run's fallback takes the under-load forms, 0/1, default 0), "keep_f" (the fallback reuses
+ * the batch pass's per-set Miller values instead of re-running the loops, 0/1, default 1), "keep_copy" (how they are
+ * copied aside: 0 hipMemcpyAsync, 1 a copy kernel; default 0), "early_release" /
  * "tail_on_msg" / "copy_stream" (run-formation experiments, 0/1, default 0: a run leaves the pipeline count when its
  * message branch is done / the group stage on the pair's high-priority message stream / the input copy on the table
  * stream),

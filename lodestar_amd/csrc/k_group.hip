@@ -298,6 +298,15 @@ STAGE_KERNEL_W(BLSGPU_WPE_GRP) void k_range_combine_lane(const uint32_t* S_in, c
 
 static inline dim3 grid_for(uint32_t n) { return dim3((n + WAVE - 1) / WAVE); }
 
+// word copy on the caller's stream (the batch pass's per-set Miller values kept aside for the fallback, runtime keep_f)
+__global__ __launch_bounds__(256) void k_copy_words(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
+                                                    size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+void launch_copy_words(uint32_t* dst, const uint32_t* src, size_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_copy_words, dim3((unsigned)std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0, s, dst, src, n);
+}
+
 void launch_group_reduce_lane(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
                               uint32_t ng, uint32_t* S, uint32_t* F, hipStream_t s) {
   if (ng) hipLaunchKernelGGL(k_group_reduce_lane, grid_for(ng), dim3(WAVE), 0, s, b, set_ranges, f_ranges, ng, S, F);

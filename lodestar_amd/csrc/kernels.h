@@ -174,6 +174,7 @@ void launch_group_sig_miller_sel(const uint32_t* S, uint32_t n_groups, const uin
 void launch_group_sig_miller(const uint32_t* S, uint32_t n_groups, uint32_t* G, hipStream_t s, bool exclusive = false,
                              bool lane = false);
 // lane-per-item forms (one lane per range / sub-group) for the fallback's many tiny ranges
+void launch_copy_words(uint32_t* dst, const uint32_t* src, size_t n, hipStream_t s);
 void launch_group_reduce_lane(const PipelineBuffers& b, const uint32_t* set_ranges, const uint32_t* f_ranges,
                               uint32_t n_groups, uint32_t* S, uint32_t* F, hipStream_t s);
 void launch_range_combine_lane(const uint32_t* S_in, const uint32_t* F_in, uint32_t n_in, const uint32_t* ranges,

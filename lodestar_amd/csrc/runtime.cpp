@@ -79,13 +79,43 @@ inline bool sync_grow() {
   }();
   return on;
 }
+// Every growth and release of a stream-ordered slot buffer holds this lock: the dispatcher threads of a device's slots
+// (and of every device) grow their buffers at the same moments -- a fresh process's first runs, and whenever the run
+// shapes change -- and the stream-ordered pool is then entered from several threads at once.  Growth is rare (buffers
+// only double), so the lock costs nothing measurable.  BLSGPU_GROW_UNLOCKED=1 (diagnostics) leaves it out.
+std::mutex g_grow_mu;
+inline bool grow_unlocked() {
+  static const bool on = [] {
+    const char* v = getenv("BLSGPU_GROW_UNLOCKED");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+// Diagnostics (BLSGPU_FB_VERIFY=1): every fallback of small jobs is re-computed and compared (run_shard)
+inline bool fb_verify() {
+  static const bool on = [] {
+    const char* v = getenv("BLSGPU_FB_VERIFY");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+inline bool grow_free() {
+  static const bool on = [] {
+    const char* v = getenv("BLSGPU_GROW_FREE");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
 template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t cap = 0;
   hipStream_t st = nullptr;  // set for slot buffers
+  std::vector<T*> retired;   // outgrown stream-ordered blocks, freed with the buffer (ensure)
   void ensure(size_t n) {
     if (n <= cap) return;
+    std::unique_lock<std::mutex> lk(g_grow_mu, std::defer_lock);
+    if (!grow_unlocked()) lk.lock();
     const size_t c = std::max<size_t>(n, cap * 2);
     if (st && sync_grow()) {
       HIPCHK(hipDeviceSynchronize());
@@ -96,7 +126,12 @@ struct DevBuf {
       HIPCHK(hipDeviceSynchronize());
       tl_async_grow++;
     } else if (st) {
-      if (p) HIPCHK(hipFreeAsync(p, st));
+      // the outgrown block is kept until the buffer is released instead of going back to the stream-ordered pool at
+      // once (BLSGPU_GROW_FREE=1: freed at once, as before): with the adaptive group sizes, whose buffer shapes change
+      // over a fresh process's first runs, the kept per-set Miller values (run_shard keep_f) were found overwritten in
+      // ~6% of fresh C5 processes.  Growth doubles, so the kept blocks add up to less than the buffer.
+      if (p && grow_free()) HIPCHK(hipFreeAsync(p, st));
+      else if (p) retired.push_back(p);
       p = nullptr;
       HIPCHK(hipMallocAsync((void**)&p, c * sizeof(T), st));
       if (poison_buffers()) HIPCHK(hipMemsetAsync(p, 0xA5, c * sizeof(T), st));
@@ -113,7 +148,11 @@ struct DevBuf {
     cap = c;
   }
   void release() {
+    std::unique_lock<std::mutex> lk(g_grow_mu, std::defer_lock);
+    if (!grow_unlocked()) lk.lock();
     if (p) (void)(st ? hipFreeAsync(p, st) : hipFree(p));
+    for (T* q : retired) (void)(st ? hipFreeAsync(q, st) : hipFree(q));
+    retired.clear();
     p = nullptr;
     cap = 0;
   }
@@ -125,6 +164,8 @@ struct HostBuf {  // pinned staging
   size_t cap = 0;
   void ensure(size_t n) {
     if (n <= cap) return;
+    std::unique_lock<std::mutex> lk(g_grow_mu, std::defer_lock);
+    if (!grow_unlocked()) lk.lock();
     if (p) HIPCHK(hipHostFree(p));
     p = nullptr;
     size_t c = std::max<size_t>(n, cap * 2);
@@ -292,6 +333,8 @@ struct Options {  // snapshot taken at the start of each call
   int64_t fb_direct_min = 1024;   // large runs under load with >= this many retried jobs check each directly (0 = never)
   int64_t fb_check6 = 2;          // those runs' lane checks: 0 one lane per check; 1 MillerLoop(-g1, S) one lane and the
                                   // final exponentiation six lanes per check (gt6.hpp); 2 both on six lanes
+  int64_t keep_f = 1;             // the fallback reuses the batch pass's per-set Miller values (0: re-runs the loops)
+  int64_t keep_copy = 0;          // how they are copied aside: 0 hipMemcpyAsync, 1 a copy kernel on the same stream
   int64_t fb_force_busy = 0;      // tests: every run's fallback takes the under-load forms
   int64_t urgent_lane = 1;        // calls with a BLSGPU_JOB_URGENT job run on the device's urgent lane
   int64_t urgent_max_sets = 512;  // larger urgent calls go to the head of the device queue instead
@@ -309,7 +352,7 @@ struct Options {  // snapshot taken at the start of each call
            coop_g2_max == o.coop_g2_max && coop_excl_max == o.coop_excl_max && rsig_spec == o.rsig_spec && spec_large == o.spec_large && spec_gsm == o.spec_gsm &&
            fb_lane_min == o.fb_lane_min && acc6_max == o.acc6_max && miller_pairs == o.miller_pairs && small_max == o.small_max &&
            fb_direct_min == o.fb_direct_min && fb_check6 == o.fb_check6 && fb_force_busy == o.fb_force_busy &&
-           group_adapt == o.group_adapt;
+           group_adapt == o.group_adapt && keep_f == o.keep_f && keep_copy == o.keep_copy;
   }
 };
 
@@ -752,7 +795,7 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
   // non-empty job, in order), so the batch pass's Miller values f_c = MillerLoop(r_c pk_c, H(m_c)) are exactly what a
   // failed group's per-job checks need.  They are copied aside before the F tree multiplies chunks in place, and the
   // fallback takes F_j = prod of its sets' kept values instead of re-running the Miller loops.
-  const bool keep_f = !merged && mk == 1 && n_chunks == n;
+  const bool keep_f = opt.keep_f && !merged && mk == 1 && n_chunks == n;
   // A small run (<= opt.small_max sets) leaves most of the chip idle whatever its kernel forms: on an idle device it takes
   // the other stream pair too (speculative MSM, parallel pubkey branch, r_i sig_i), and its fallback checks stay
   // cooperative (latency) instead of lane-per-check (throughput).
@@ -1102,7 +1145,9 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
     else
       launch_miller_acc_auto(pb, merged, sm, mk, opt.miller_lanes, opt.acc6_max, opt.miller_pairs != 0);
     end(5, sm);
-    if (keep_f)
+    if (keep_f && opt.keep_copy == 1)
+      launch_copy_words(sl.d_fkeep.p, pb.f_chunk, (size_t)stride * W_FP12, sm);
+    else if (keep_f)
       HIPCHK(hipMemcpyAsync(sl.d_fkeep.p, pb.f_chunk, (size_t)stride * W_FP12 * 4, hipMemcpyDeviceToDevice, sm));
     const uint32_t* d_franges = reinterpret_cast<uint32_t*>(din + o_franges);
     beg(6, sm);
@@ -1400,6 +1445,59 @@ int run_shard(Device& d, Slot& sl, const blsgpu_batch& b, const Shard& sh, int8_
       HIPCHK(hipEventRecord(sl.done, sfb));
       HIPCHK(hipEventSynchronize(sl.done));
       for (uint32_t k = 0; k < ns; k++) jr[retry[sel[k]]] = sl.h_ok.p[k] ? 1 : 0;
+    }
+    if (fb_verify() && small_jobs) {
+      // Diagnostics (BLSGPU_FB_VERIFY=1): the fallback again from its inputs into fresh buffers once the device is idle
+      // -- r_i sig_i, S_j / F_j, one cooperative check per job -- compared with the first pass's S_j, F_j (as they
+      // are now in dS / dF), its uploaded lists, its results as read and as they are now in d_ok, and the answers.
+      HIPCHK(hipDeviceSynchronize());
+      const size_t wS = (size_t)W_G2J * nr, wF = (size_t)W_FP12 * nr;
+      std::vector<uint32_t> S1(wS), F1(wF), S2(wS), F2(wF), L(o_sel);
+      std::vector<uint8_t> ok_now(sel.size() + 1), ok2(nr);
+      HIPCHK(hipMemcpy(S1.data(), dS, wS * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(F1.data(), dF, wF * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(L.data(), sl.d_list.p, o_sel * 4, hipMemcpyDeviceToHost));
+      if (!sel.empty()) HIPCHK(hipMemcpy(ok_now.data(), sl.d_ok.p, sel.size(), hipMemcpyDeviceToHost));
+      uint32_t *t_rs = nullptr, *t_S = nullptr, *t_F = nullptr;
+      uint8_t* t_ok = nullptr;
+      HIPCHK(hipMalloc((void**)&t_rs, (size_t)stride * 9 * W_G2J * 4));
+      HIPCHK(hipMalloc((void**)&t_S, wS * 4));
+      HIPCHK(hipMalloc((void**)&t_F, wF * 4));
+      HIPCHK(hipMalloc((void**)&t_ok, nr));
+      PipelineBuffers pq = pr;
+      pq.rsig = t_rs;
+      pq.scal_tab = t_rs + (size_t)stride * W_G2J;
+      launch_sig_scale(pq, (uint32_t)rset.size(), sfb, sl.d_list.p + o_rset);
+      launch_group_reduce_lane(pq, sl.d_list.p, sl.d_list.p + 2 * (size_t)nr, nr, t_S, t_F, sfb);
+      launch_group_check(t_S, t_F, nr, t_ok, sfb, nullptr, 0, nullptr, false, false);
+      HIPCHK(hipStreamSynchronize(sfb));
+      HIPCHK(hipMemcpy(S2.data(), t_S, wS * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(F2.data(), t_F, wF * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(ok2.data(), t_ok, nr, hipMemcpyDeviceToHost));
+      (void)hipFree(t_rs), (void)hipFree(t_S), (void)hipFree(t_F), (void)hipFree(t_ok);
+      // S / F are stored structure-of-arrays (word w of job q at w * nr + q)
+      uint32_t sdiff = 0, fdiff = 0, vdiff = 0, stale = 0, ldiff = 0, first_v = UINT32_MAX, last_v = 0;
+      for (uint32_t q = 0; q < nr; q++) {
+        bool ds = false, df = false;
+        for (size_t w = 0; w < W_G2J && !ds; w++) ds = S1[w * nr + q] != S2[w * nr + q];
+        for (size_t w = 0; w < W_FP12 && !df; w++) df = F1[w * nr + q] != F2[w * nr + q];
+        sdiff += ds, fdiff += df;
+        if ((jr[retry[q]] == 1) != (ok2[q] != 0)) {
+          vdiff++;
+          first_v = std::min(first_v, q);
+          last_v = q;
+        }
+      }
+      for (size_t k = 0; k < o_sel; k++) ldiff += L[k] != hl[k];
+      for (size_t k = 0; k < sel.size(); k++) stale += (ok_now[k] != 0) != (sl.h_ok.p[k] != 0);
+      if (vdiff || sdiff || fdiff || stale || ldiff)
+        fprintf(stderr, "[blsgpu fbverify] %u-set run, %u retried jobs (nsub %u, direct %d, busy %d, keep_f %d, rsig_spec "
+                "%d, spec %d, coop %d, lanes %d): answers that differ on re-check %u (q %u-%u), S_j differ %u, F_j differ "
+                "%u, results read vs now %u, list words %zu\n", n, nr, nsub, (int)direct, (int)busy, (int)keep_f,
+                (int)rsig_spec, (int)spec, (int)coop, (int)lane_checks((uint32_t)sel.size()), vdiff, first_v, last_v,
+                sdiff, fdiff, stale, (size_t)ldiff);
+      else
+        fprintf(stderr, "[blsgpu fbverify] ok: %u-set run, %u retried jobs\n", n, nr);
     }
   }
   // a failed group whose clean jobs all verify on their own: its batch equation was computed wrong (the random
@@ -2616,6 +2714,10 @@ int blsgpu_set_option(blsgpu_ctx* ctx, const char* key, int64_t value) {
     ctx->opt.fb_lane_min = value;
   } else if (k == "fb_force_busy") {
     ctx->opt.fb_force_busy = value != 0;
+  } else if (k == "keep_f") {
+    ctx->opt.keep_f = value != 0;
+  } else if (k == "keep_copy") {
+    ctx->opt.keep_copy = value != 0;
   } else if (k == "urgent_lane") {
     ctx->opt.urgent_lane = value != 0;
   } else if (k == "urgent_max_sets") {
@@ -2741,6 +2843,8 @@ int blsgpu_get_option(const blsgpu_ctx* cctx, const char* key, int64_t* value) {
   else if (k == "fb_direct_min") *value = o.fb_direct_min;
   else if (k == "fb_check6") *value = o.fb_check6;
   else if (k == "fb_force_busy") *value = o.fb_force_busy;
+  else if (k == "keep_f") *value = o.keep_f;
+  else if (k == "keep_copy") *value = o.keep_copy;
   else if (k == "urgent_lane") *value = o.urgent_lane;
   else if (k == "urgent_max_sets") *value = o.urgent_max_sets;
   else if (k == "urgent_excl") *value = o.urgent_excl;

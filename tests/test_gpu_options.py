@@ -14,7 +14,7 @@ KEYS = {
     "merge_wait_us": (1000, -1), "idle_wait_us": (100, -1), "lane_tail_min": (1, -1), "lane_tail_parts": (1, 4),
     "merge_balance": (1, None), "early_release": (1, None), "tail_on_msg": (1, None), "copy_stream": (1, None),
     "coop_max": (256, -1), "coop_g2_max": (1024, -1), "coop_excl_max": (128, -1), "rsig_spec": (0, None), "spec_large": (0, None), "spec_gsm": (1, None),
-    "fb_lane_min": (64, -1), "fb_direct_min": (512, -1), "fb_check6": (1, 3), "fb_force_busy": (1, None),
+    "fb_lane_min": (64, -1), "fb_direct_min": (512, -1), "fb_check6": (1, 3), "fb_force_busy": (1, None), "keep_f": (0, None), "keep_copy": (1, None),
     "route_split_sets": (8192, 0), "acc6_max": (4096, -1), "small_max": (2048, -1), "serial": (1, None),
     "profile": (1, None), "max_devices": (1, 0),
     "urgent_lane": (0, None), "urgent_max_sets": (64, -1), "urgent_excl": (1, None), "urgent_wait_us": (0, -1), "group_adapt": (1, None),
