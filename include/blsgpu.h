@@ -166,8 +166,9 @@ int blsgpu_submit(blsgpu_ctx* ctx, const blsgpu_batch* batch, int8_t* job_result
 /* Tunables ("slots" may not be changed from a done callback: BLSGPU_ERR_ARGS): "group_sets" (sets per batch group before a new one opens, default 1024), "group_adapt"
  * (while a device sees invalid sets, its batch groups shrink to the size that minimises the expected work of a group's
  * final exponentiation against re-checking a failed group's clean jobs -- 32 sets at 1% invalid, group_sets when all
- * are valid; 0/1, default 0: experimental -- fresh processes verifying C5-like calls answered false for valid jobs in
- * ~8% of runs while the group sizes moved, root cause not found), "slots" (runtime slots
+ * are valid; 0/1, default 1.  Until the runtime stopped returning outgrown slot buffers to the stream-ordered pool
+ * during operation, fresh processes verifying C5-like calls with it answered false for valid jobs in ~6% of runs),
+ * "slots" (runtime slots
  * per device, 1..64; default by hardware queues), "max_devices" (devices one call may shard over, default all),
  * "dedupe" (message dedupe + same-message pairing, 0/1, default 1), "miller_k" (pairings per Miller
  * accumulator sharing its Fp12 squarings, 1..64; default 0 = by run size: 1 below 131072 pairings, 2 below

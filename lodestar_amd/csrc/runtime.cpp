@@ -340,8 +340,8 @@ struct Options {  // snapshot taken at the start of each call
   int64_t urgent_max_sets = 512;  // larger urgent calls go to the head of the device queue instead
   int64_t urgent_excl = 0;        // urgent runs may use the exclusive-CU padding of the cooperative kernels
   int64_t urgent_wait_us = 300;   // the urgent dispatcher lingers this long for more urgent calls of a burst
-  int64_t group_adapt = 0;        // batch groups shrink below group_sets while the device sees invalid sets (off:
-                                  // wrong answers in ~8% of fresh C5 processes while the sizes move)
+  int64_t group_adapt = 1;        // batch groups shrink below group_sets while the device sees invalid sets (DESIGN
+                                  // §5.2: safe once outgrown buffers stay allocated, DevBuf::ensure)
   bool same_run(const struct Options& o) const {
     return group_sets == o.group_sets && profile == o.profile && dedupe == o.dedupe && miller_k == o.miller_k &&
            group_policy == o.group_policy && serial == o.serial && miller_lanes == o.miller_lanes &&

@@ -17,7 +17,7 @@ KEYS = {
     "fb_lane_min": (64, -1), "fb_direct_min": (512, -1), "fb_check6": (1, 3), "fb_force_busy": (1, None), "keep_f": (0, None), "keep_copy": (1, None),
     "route_split_sets": (8192, 0), "acc6_max": (4096, -1), "small_max": (2048, -1), "serial": (1, None),
     "profile": (1, None), "max_devices": (1, 0),
-    "urgent_lane": (0, None), "urgent_max_sets": (64, -1), "urgent_excl": (1, None), "urgent_wait_us": (0, -1), "group_adapt": (1, None),
+    "urgent_lane": (0, None), "urgent_max_sets": (64, -1), "urgent_excl": (1, None), "urgent_wait_us": (0, -1), "group_adapt": (0, None),
     # stream creation options: the fixture's context has made no call yet, so they still take values
     "urgent_cus": (16, 12), "urgent_isolate": (2, 4), "blocking_sync": (0, 2), "pipeline_prio": (0, 2),
 }
