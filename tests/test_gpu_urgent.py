@@ -88,7 +88,7 @@ def test_urgent_calls_overtake_a_gossip_flood(env):
     """FLOOD_CALLS x 16,384-set gossip calls are queued first (blsgpu_submit, asynchronous), then -- 30 ms later, within
     microseconds of each other -- the urgent calls (valid, wrong message, malformed signature, 3-set jobs) and the same
     calls without the urgent flag: every urgent call gives the oracle's answer on the urgent lane, and the burst runs in at
-    most two lane runs; the finish times against the flood's are printed."""
+    most three lane runs; the finish times against the flood's are printed."""
     ctx, sks, pks, flood = env
     calls = [urgent_call(sks, idx, kinds, 100 + t) for t, (idx, kinds, _) in enumerate(URGENT_CASES)]
     seeds = [bench.SEED + 100 + t for t in range(len(calls))]
@@ -115,7 +115,8 @@ def test_urgent_calls_overtake_a_gossip_flood(env):
         assert int(res2[0]) == wants[t] and st2.urgent_lane == 0
     runs = sum(1.0 / p[1].run_calls for p in u)  # a run of k calls reports run_calls == k in each of them
     print(f"the urgent burst ran as {runs:.2f} lane runs ({[p[1].run_calls for p in u]})")
-    assert runs <= 2.01, "the urgent burst was not merged into lane runs"
+    # five calls submitted within microseconds: merged into at most three lane runs (1-2 in every run seen so far)
+    assert runs <= 3.01, "the urgent burst was not merged into lane runs"
     # The finish times are printed, not asserted.  The lane never waits in the FIFO, but under the flood each of a lane
     # run's dependent kernels waits for free SIMDs, i.e. for flood waves to retire.  The burst usually
     # finishes ~50 ms after submission, long before the flood drains.  In one run of this test it took ~230 ms and
